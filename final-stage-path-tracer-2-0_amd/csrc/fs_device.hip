@@ -1,0 +1,1239 @@
+// fs_device.hip — gfx950 kernels of the path-trace hot path + the C ABI.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (bit parity with
+// the reference needs unfused float ops; the BVH slab test, which only
+// culls, uses explicit fmaf).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "fs_kernels.h"
+#include "fs_scene.h"
+#include "fs_trace.h"
+
+namespace fs {
+namespace dev {
+
+struct Ray {
+  f3 start, stop, dir;
+};
+
+struct Hit {
+  float t;
+  f3 p, n;
+  int32_t mat;
+  int32_t obj;
+  uint32_t tri;  // global triangle index of a mesh hit
+  float u, v;
+};
+
+__device__ __forceinline__ bool zero_len(const Ray& r) {  // trace.cpp:16
+  return cmp_eps(length(r.dir), 0.0f, kEpsilon);
+}
+
+// intersect.cpp:728-744 — two-sided plane test, t in [0,1].
+__device__ __forceinline__ bool ray_plane(f4 p, const Ray& r, float& t, f3& point) {
+  float ts = (p.x * r.dir.x + p.y * r.dir.y + p.z * r.dir.z);
+  if (!cmp_eps(ts, 0.0f, kEpsilon)) {
+    float ns = -(p.x * r.start.x + p.y * r.start.y + p.z * r.start.z + p.w);  // (...) * -1.0
+    float tt = ns / ts;
+    if (tt >= 0 && tt <= 1) {
+      t = tt;
+      point = r.start + r.dir * tt;
+      return true;
+    }
+  }
+  return false;
+}
+
+// intersect.cpp:421-488 (the zero-length branch never reports a hit through
+// SphericalObject::Trace, object.cpp:23-36, so callers skip it).
+__device__ __forceinline__ bool ray_sphere(f3 c, float radius, const Ray& r, float& t, f3& p, f3& n) {
+  f3 o = r.start - c;
+  float a = dot(r.dir, r.dir);
+  float b = 2 * (dot(o, r.dir));
+  float cc = dot(o, o) - radius * radius;
+  float d = b * b - 4 * a * cc;
+  if (d < 0) return false;
+  float tt;
+  if (length(o) <= radius)
+    tt = (-b + fsqrt(d)) / (2 * a);
+  else
+    tt = (-b - fsqrt(d)) / (2 * a);
+  if (tt < 0 || tt > 1) return false;
+  t = tt;
+  p = r.start + r.dir * tt;
+  n = normalize(p - c);
+  return true;
+}
+
+// intersect.cpp:490-529
+__device__ __forceinline__ bool ref_slab(float s, float v, float mn, float mx, float& pn, float& pf) {
+  if (cmp_eps(v, 0.0f, kEpsilon)) return !(s < mn || s > mx);
+  float t1 = (mn - s) / v;
+  float t2 = (mx - s) / v;
+  if (t1 > t2) {
+    float tt = t1;
+    t1 = t2;
+    t2 = tt;
+  }
+  if (t1 > pn) pn = t1;
+  if (t2 < pf) pf = t2;
+  return true;
+}
+// intersect.cpp:531-597 (only the parameter is consumed)
+__device__ __forceinline__ bool ref_bounds_worker(f3 mn, f3 mx, f3 s, f3 e, float& param) {
+  f3 v = e - s;
+  float fnear = -kInfinity, ffar = kInfinity;
+  if (!ref_slab(s.x, v.x, mn.x, mx.x, fnear, ffar)) return false;
+  if (!ref_slab(s.y, v.y, mn.y, mx.y, fnear, ffar)) return false;
+  if (!ref_slab(s.z, v.z, mn.z, mx.z, fnear, ffar)) return false;
+  if (fnear > ffar) return false;
+  if (ffar < 0 || fnear < 0 || fnear > 1) return false;
+  param = fnear;
+  return true;
+}
+__device__ __forceinline__ bool in_bounds(f3 mn, f3 mx, f3 p) {  // intersect.cpp:16-24
+  return p.x >= mn.x && p.x <= mx.x && p.y >= mn.y && p.y <= mx.y && p.z >= mn.z && p.z <= mx.z;
+}
+// intersect.cpp:599-654
+__device__ __forceinline__ bool ref_ray_bounds(f3 mn, f3 mx, const Ray& r, bool zl, float& param) {
+  if (zl) {
+    if (in_bounds(mn, mx, r.start)) {
+      param = 0.0f;
+      return true;
+    }
+    return false;
+  }
+  bool si = in_bounds(mn, mx, r.start);
+  if (si && in_bounds(mn, mx, r.stop)) {
+    param = 0.0f;
+    return true;
+  }
+  if (si) {
+    if (ref_bounds_worker(mn, mx, r.stop, r.start, param)) {
+      param = 1.0f - param;
+      return true;
+    }
+    return false;
+  }
+  return ref_bounds_worker(mn, mx, r.start, r.stop, param);
+}
+
+// intersect.cpp:96-129 + 146-177: planar map, then barycentrics.
+__device__ __forceinline__ void planar_bary(f4 pl, f3 v0, f3 v1, f3 vp, float& u, float& v) {
+  float ax = fabsf(pl.x), ay = fabsf(pl.y), az = fabsf(pl.z);
+  if (ax >= ay) {
+    if (ax >= az) {
+      v0.x = v1.x = vp.x = 0;
+    } else {
+      v0.z = v1.z = vp.z = 0;
+    }
+  } else {
+    if (ay >= az) {
+      v0.y = v1.y = vp.y = 0;
+    } else {
+      v0.z = v1.z = vp.z = 0;
+    }
+  }
+  float d00 = dot(v0, v0), d01 = dot(v0, v1), d02 = dot(v0, vp);
+  float d11 = dot(v1, v1), d12 = dot(v1, vp);
+  float inv = 1 / (d00 * d11 - d01 * d01);
+  u = (d11 * d02 - d01 * d12) * inv;
+  v = (d00 * d12 - d01 * d02) * inv;
+}
+
+struct TriData {
+  f3 p1, p2, p3;
+  f4 pl;
+  uint32_t face;
+};
+__device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
+  const float4* q = reinterpret_cast<const float4*>(T + i);
+  float4 a = q[0], b = q[1], c = q[2], d = q[3];
+  TriData t;
+  t.p1 = mk3(a.x, a.y, a.z);
+  t.p2 = mk3(b.x, b.y, b.z);
+  t.p3 = mk3(c.x, c.y, c.z);
+  t.pl = mk4(d.x, d.y, d.z, d.w);
+  t.face = __float_as_uint(a.w);
+  return t;
+}
+
+// intersect.cpp:357-419 (non-zero-length branch)
+__device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t, f3& p, float& u, float& v) {
+  float tt;
+  f3 pp;
+  if (!ray_plane(T.pl, r, tt, pp)) return false;
+  float uu, vv;
+  planar_bary(T.pl, T.p2 - T.p1, T.p3 - T.p1, pp - T.p1, uu, vv);
+  if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
+    t = tt;
+    p = pp;
+    u = uu;
+    v = vv;
+    return true;
+  }
+  return false;
+}
+// intersect.cpp:320-346 with point_in_plane's vector4 promotion (:45-47):
+// the live test is n.p + w + w.
+__device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, float& v) {
+  float d4 = T.pl.x * pt.x + T.pl.y * pt.y + T.pl.z * pt.z + T.pl.w * 1.0f;
+  if (!cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) return false;
+  float uu, vv;
+  planar_bary(T.pl, T.p2 - T.p1, T.p3 - T.p1, pt - T.p1, uu, vv);
+  if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
+    u = uu;
+    v = vv;
+    return true;
+  }
+  return false;
+}
+
+template <bool COUNT>
+struct Tally {
+  uint32_t nodes = 0, tris = 0, prims = 0;
+};
+
+// Traverses one mesh's BVH2 (conservative culling) and applies the
+// reference leaf rule: a face replaces the current hit iff t < best, or on an
+// exact tie within the same mesh iff its face index is lower (the order in
+// which mesh.cpp:89-110 would meet the two faces in one octree leaf).
+template <bool COUNT>
+__device__ __forceinline__ void traverse_mesh(const DevScene& S, uint32_t root, int32_t oi, int32_t mat,
+                                              const Ray& r, bool zl, Hit& h, uint32_t* __restrict__ stk,
+                                              Tally<COUNT>& tally) {
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
+  uint32_t w = root;
+  uint32_t sp = 0;
+  for (;;) {
+    if (!(w & kLeafBit)) {
+      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+      float4 X = q[0], Y = q[1], Z = q[2];
+      uint4 C = reinterpret_cast<const uint4*>(q)[3];
+      if (COUNT) tally.nodes++;
+      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+      bool h0, h1;
+      float t0, t1;
+      if (!zl) {
+        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
+        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
+        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
+        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
+        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
+        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
+        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
+        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
+        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
+        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
+        h0 = n0 <= f0;
+        h1 = n1 <= f1;
+        t0 = n0;
+        t1 = n1;
+      } else {  // a point: visit every box that contains it
+        f3 s = r.start;
+        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
+        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
+        t0 = t1 = 0.0f;
+      }
+      if (h0 && h1) {
+        uint32_t nearw = t1 < t0 ? C.y : C.x;
+        uint32_t farw = t1 < t0 ? C.x : C.y;
+        stk[sp * kBlock] = farw;
+        sp++;
+        w = nearw;
+        continue;
+      }
+      if (h0) {
+        w = C.x;
+        continue;
+      }
+      if (h1) {
+        w = C.y;
+        continue;
+      }
+    } else {
+      uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
+      for (uint32_t i = 0; i < cnt; i++) {
+        uint32_t ti = first + i;
+        TriData T = load_tri(S.tris, ti);
+        uint32_t face = T.face;
+        if (COUNT) tally.tris++;
+        float t, u, v;
+        f3 p;
+        bool hit;
+        if (!zl) {
+          hit = ray_tri(T, r, t, p, u, v);
+        } else {
+          hit = point_in_tri(T, r.start, u, v);
+          t = 0.0f;
+          p = r.start;
+        }
+        if (hit) {
+          bool better = t < h.t || (t == h.t && h.obj == oi && face < S.tris[h.tri].face);
+          if (better) {
+            h.t = t;
+            h.p = p;
+            h.n = xyz(T.pl);
+            h.mat = mat;
+            h.obj = oi;
+            h.tri = ti;
+            h.u = u;
+            h.v = v;
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    w = stk[sp * kBlock];
+  }
+}
+
+// Scene::Trace (scene.cpp:227-249) over the object list.
+template <bool COUNT>
+__device__ bool scene_trace(const DevScene& S, const Ray& r, Hit& h, uint32_t* __restrict__ stk,
+                            Tally<COUNT>& tally) {
+  h.t = 2.0f;
+  h.p = mk3(0, 0, 0);
+  h.n = mk3(0, 0, 0);
+  h.mat = -1;
+  h.obj = -1;
+  h.tri = 0;
+  h.u = h.v = 0.0f;
+  bool zl = zero_len(r);
+  bool detected = false;
+  for (uint32_t oi = 0; oi < S.num_objects; ++oi) {
+    const DevObject* __restrict__ o = S.objects + oi;
+    int32_t kind = o->kind, mat = o->mat;
+    const float* d = o->d;
+    if (kind == FS_OBJ_MESH) {
+      if (!o->i2) continue;
+      float np;
+      // MeshBvhNode::Trace root test (mesh.cpp:79-83), restated exactly: the
+      // reference skips the mesh when the root box "param" exceeds the best.
+      if (!ref_ray_bounds(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, np) || np > h.t) continue;
+      float before = h.t;
+      int32_t before_obj = h.obj;
+      traverse_mesh<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, mat, r, zl, h, stk, tally);
+      if (h.t != before || h.obj != before_obj) detected = true;
+      continue;
+    }
+    if (zl) continue;  // analytic objects never report a hit for a zero-length ray
+    if (COUNT) tally.prims++;
+    float t;
+    f3 p, n;
+    if (kind == FS_OBJ_SPHERE) {  // object.cpp:23-36
+      if (ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n) && t < h.t) {
+        h.t = t; h.p = p; h.n = n; h.mat = mat; h.obj = (int32_t)oi;
+        detected = true;
+      }
+    } else if (kind == FS_OBJ_PLANE) {  // object.cpp:59-73
+      f4 pl = mk4(d[0], d[1], d[2], d[3]);
+      if (ray_plane(pl, r, t, p) && t < h.t) {
+        h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
+        detected = true;
+      }
+    } else if (kind == FS_OBJ_DISC) {  // object.cpp:97-113
+      f4 pl = mk4(d[0], d[1], d[2], d[3]);
+      if (ray_plane(pl, r, t, p)) {
+        if (length(mk3(d[4], d[5], d[6]) - p) <= d[7] && t < h.t) {
+          h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
+          detected = true;
+        }
+      }
+    } else if (kind == FS_OBJ_QUAD_ONWH) {  // object.cpp:213-237
+      f4 pl = mk4(d[0], d[1], d[2], d[3]);
+      if (ray_plane(pl, r, t, p)) {
+        f3 ph = p - mk3(d[4], d[5], d[6]);
+        float td = dot(mk3(d[12], d[13], d[14]), ph);
+        float bd = dot(mk3(d[9], d[10], d[11]), ph);
+        if (!(fabsf(bd) > d[7] || fabsf(td) > d[8]) && t < h.t) {
+          h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
+          detected = true;
+        }
+      }
+    } else if (kind == FS_OBJ_CUBOID) {  // object.cpp:126-165
+      for (uint32_t i = 0; i < 6; i++) {
+        f4 pl = mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
+        if (ray_plane(pl, r, t, p) && t < h.t) {
+          bool ok = true;
+          for (uint32_t j = 0; j < 6; j++) {
+            if (i / 2 != j / 2 && plane_dist(mk4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]), p) > 0.0f) {
+              ok = false;
+              break;
+            }
+          }
+          if (ok) {
+            h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
+            detected = true;
+          }
+        }
+      }
+    }
+  }
+  if (detected && h.obj >= 0 && S.objects[h.obj].kind == FS_OBJ_MESH && S.objects[h.obj].i1) {
+    // MeshObject::Trace interpolated (unnormalised) normal, mesh.cpp:289-298
+    const float4* nq = S.tri_normals + 3 * (size_t)h.tri;
+    float4 a = nq[0], b = nq[1], c = nq[2];
+    f3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(b.x, b.y, b.z), n2 = mk3(c.x, c.y, c.z);
+    h.n = n0 + (n1 - n0) * h.u + (n2 - n0) * h.v;
+  }
+  f4 cp = plane_np(h.n, h.p);
+  if (plane_dist(cp, r.start) < 0.0f) h.n = h.n * (float)-1.0;
+  return detected;
+}
+
+// normal_sphere (normal.cpp:29-105)
+__device__ __forceinline__ f3 table_normal(const DevScene& S, uint64_t& rng) {
+  float4 q = S.table[rng_table_index(rng)];
+  return mk3(q.x, q.y, q.z);
+}
+__device__ __forceinline__ f3 random_reflection(const DevScene& S, f3 inc, f3 n, float solid, uint64_t& rng) {
+  f3 rd = reflect(inc, n);
+  f3 dd = table_normal(S, rng);
+  if (dot(dd, n) < 0.0f) dd = dd * -1.0f;
+  float interp = solid / kPi;
+  f3 refl = normalize(dd * interp + rd * (float)(1.0 - (double)interp));
+  if (dot(refl, n) < 0.0f) refl = refl * -1.0f;
+  return refl;
+}
+__device__ __forceinline__ f3 random_refraction(const DevScene& S, f3 inc, f3 n, float solid, float index,
+                                                uint64_t& rng) {
+  float half = solid / 2.0f;
+  float delta = (rng_float_range(rng, -1.0f, 1.0f)) * half;
+  f3 refl = cmp_eps(index, 1.0f, kEpsilon) ? inc : refract(inc, n, index);
+  refl = normalize(refl);
+  f3 axis = table_normal(S, rng);
+  if (dot(axis, n) < 0.0f) axis = axis * -1.0f;
+  if (cmp_eps(solid, kPi, kEpsilon)) return axis;
+  if (cmp_eps(solid, 0.0f, kEpsilon)) return refl;
+  return rotate(refl, cosf(delta), sinf(delta), axis);
+}
+
+// Material::Reflection (material.cpp)
+__device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, f3 view, f3 n, uint64_t& rng) {
+  switch (m.kind) {
+    case FS_MAT_LIGHT:
+      return mk3(0, 0, 0);
+    case FS_MAT_DIFFUSE:
+      return random_reflection(S, view, n, kPi, rng);
+    case FS_MAT_METAL:
+      return random_reflection(S, view, n, kPi * m.roughness, rng);
+    case FS_MAT_MIRROR:
+      return reflect(view, n);
+    case FS_MAT_GLASS:
+      if (rng_float(rng) < m.reflectivity) return random_reflection(S, view, n, kPi * m.frost, rng);
+      return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
+    case FS_MAT_LIQUID:
+      if (rng_float(rng) < m.reflectivity) return reflect(view, n);
+      return refract(view, n, m.index);
+    case FS_MAT_CERAMIC:
+    case FS_MAT_GLOW:
+      if (rng_float(rng) < 0.1f) return random_reflection(S, view, n, 0.0f, rng);
+      return random_reflection(S, view, n, (float)((double)kPi * (1.0 - (double)m.shininess)), rng);
+    default:  // FS_MAT_FOG
+      return view;
+  }
+}
+__device__ __forceinline__ bool mat_will_use(const fs_material& m, f3 r, f3 n) {
+  switch (m.kind) {
+    case FS_MAT_LIGHT:
+      return false;
+    case FS_MAT_DIFFUSE:
+      return dot(r, n) > kDiffuseContrib;
+    case FS_MAT_METAL:
+      return m.roughness <= kRoughnessThr || dot(r, n) > kDiffuseContrib;
+    default:
+      return true;
+  }
+}
+
+struct Aov {
+  f3 normal;
+  float depth;
+  uint64_t id;
+};
+
+__device__ __forceinline__ uint32_t mat_of(uint32_t lo, uint32_t hi, int k) {
+  return (k < 4 ? (lo >> (8 * k)) : (hi >> (8 * (k - 4)))) & 0xFFu;
+}
+
+// One sample = TracePixel (engine.cpp:161-164) after the ray generation of
+// engine.cpp:210-244. Returns the TraceResult colour.
+template <bool COUNT>
+__device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, float fy, uint64_t rng, Aov& aov,
+                           uint32_t* __restrict__ stk, float2* __restrict__ lvl, Tally<COUNT>& tally,
+                           uint32_t& segments) {
+  // ---- camera ray (engine.cpp:210-244)
+  float jx = (float)((double)rng_float(rng) - 0.5);
+  float jy = (float)((double)rng_float(rng) - 0.5);
+  float xd = (float)((double)C.hpw * ((double)((fx + jx) / (C.width - 1)) * 2.0 - 1.0));
+  float yd = (float)((double)C.hph * ((double)((fy + jy) / (C.height - 1)) * 2.0 - 1.0));
+  f3 stop = C.proj_origin + C.right * xd + C.up * yd;
+  Ray r;
+  r.start = C.origin;
+  r.stop = stop;
+  r.dir = stop - C.origin;
+  if (C.aperture > 0.0f) {
+    float ft;
+    f3 fp;
+    if (ray_plane(C.focal, r, ft, fp)) {
+      float ang = (float)((double)rng_float(rng) * 2.0 * (double)kPi);
+      float mag = fsqrt(rng_float(rng)) * C.aperture;
+      f3 off = C.right * cosf(ang) * mag + C.up * sinf(ang) * mag;
+      r.start = r.start + off;
+      r.stop = r.start + normalize(fp - r.start) * C.z_far;
+      r.dir = r.stop - r.start;
+    }
+  }
+
+  // ---- forward pass: TraceStep recursion descending (engine.cpp:59-138)
+  uint32_t mats_lo = 0, mats_hi = 0;
+  f3 L = mk3(0, 0, 0);
+  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
+  int top = -1;
+  for (uint32_t depth = 0;; depth++) {
+    if (depth >= kMaxDepth) {
+      L = mk3(0, 0, 0);
+      break;
+    }
+    if (C.fast_render && depth > 1) {
+      L = mk3(1, 1, 1);
+      break;
+    }
+    segments++;
+    Hit h;
+    if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
+      if (depth == 1) lp0 = r.stop;
+      L = mk3(S.sky_r, S.sky_g, S.sky_b);
+      if (depth == 0) {
+        aov.normal = normalize(r.dir);
+        aov.id = S.sky_id;
+        aov.depth = C.z_far;
+      }
+      break;
+    }
+    if (depth == 1) lp0 = h.p;
+    const fs_material& m = S.materials[h.mat];
+    int32_t kind = m.kind;
+    f3 view = normalize(h.p - r.start);
+    f3 refl = mat_reflection(S, m, view, h.n, rng);
+    float c = fmaxf(0.0f, dot(h.n, refl));
+    float ds = 0.0f;
+    if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
+      f3 hv = normalize(view * (float)-1.0 + refl);
+      ds = (float)pow((double)dot(hv, h.n), 50.0);
+    }
+    lvl[depth * kBlock] = make_float2(c, ds);
+    if (depth < 4)
+      mats_lo |= (uint32_t)h.mat << (8 * depth);
+    else
+      mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
+    top = (int)depth;
+    if (depth == 0) {
+      p0 = h.p;
+      aov.normal = h.n;
+      aov.id = m.id;
+      aov.depth = length(r.start - h.p);
+    }
+    Ray nr;  // engine.cpp:120-127
+    nr.start = h.p;
+    nr.stop = h.p + refl * C.z_far;
+    nr.dir = nr.stop - nr.start;
+    f3 off = refl * kStepOffset;
+    nr.start = nr.start + off;
+    nr.dir = nr.dir - off;
+    if (!mat_will_use(m, refl, h.n)) {
+      L = mk3(0, 0, 0);
+      break;
+    }
+    r = nr;
+  }
+
+  // ---- backward pass: Material::Sample in the recursion's return order
+  for (int k = top; k >= 0; --k) {
+    const fs_material& m = S.materials[mat_of(mats_lo, mats_hi, k)];
+    float2 cs = lvl[k * kBlock];
+    f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
+    switch (m.kind) {
+      case FS_MAT_LIGHT:
+        L = mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
+        break;
+      case FS_MAT_DIFFUSE:
+        L = (dif * L) * cs.x;
+        break;
+      case FS_MAT_METAL: {
+        f3 dc = (dif * L) * cs.x;
+        f3 rc = dif * L;
+        L = dc * m.roughness + rc * (float)(1.0 - (double)m.roughness);
+        break;
+      }
+      case FS_MAT_MIRROR:
+      case FS_MAT_GLASS:
+      case FS_MAT_LIQUID:
+        L = L * dif;
+        break;
+      case FS_MAT_CERAMIC:
+      case FS_MAT_GLOW: {
+        f3 dc = (dif * L) * cs.x;
+        L = L * cs.y + dc * (float)(1.0 - (double)cs.y);
+        if (m.kind == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
+        break;
+      }
+      default:  // FS_MAT_FOG (material.cpp:319-339)
+        if (k == 0) {
+          float dist = length(p0 - lp0);
+          float x = (dist * dist) * m.density * 0.00005f;
+          float mx = (0.0f < x) ? x : 0.0f;
+          float th = (mx < 0.0f) ? 0.0f : (mx > 1.0f ? 1.0f : mx);
+          if (rng_float(rng) < th) L = dif;
+        }
+        break;
+    }
+  }
+  if (top >= 0) {  // engine.cpp:147-151
+    const fs_material& m0 = S.materials[mat_of(mats_lo, mats_hi, 0)];
+    if (length(L) > 10.0f && m0.kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
+  }
+  return L;
+}
+
+__device__ __forceinline__ uint8_t gamma8(float c) {  // frame.cpp:67-71
+  float s = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
+  return (uint8_t)(255.0 * pow((double)s, 1.0 / 2.2) + 0.5);
+}
+
+// One block = one wave64 = one 8x8 pixel block of an owned tile; each lane
+// walks its pixel's samples in order, applying DisplayFrame::WritePixel's
+// running mean after each (frame.cpp:53-63).
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevFrame F, Launch P,
+                                                         DevCounters* __restrict__ counters) {
+  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  __shared__ float2 lvl_all[kMaxDepth * kBlock];
+  const uint32_t lane = threadIdx.x;
+  uint32_t* stk = stk_all + lane;
+  float2* lvl = lvl_all + lane;
+
+  const uint32_t micro_per_side = P.tile_size / 8;
+  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t owned = blockIdx.x / micro_per_tile;
+  const uint32_t micro = blockIdx.x % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const uint32_t x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+  const uint32_t y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  if (x >= F.width || y >= F.height) return;
+
+  const size_t pix = (size_t)y * F.width + x;
+  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
+  uint32_t n = F.count[pix];
+  Aov aov;
+  aov.normal = mk3(0, 0, 0);
+  aov.depth = 0.0f;
+  aov.id = 0;
+  Tally<COUNT> tally;
+  uint32_t segments = 0;
+  for (uint32_t s = 0; s < P.spp; s++) {
+    uint64_t rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
+    f3 L = trace_sample<COUNT>(S, C, (float)x, (float)y, rng, aov, stk, lvl, tally, segments);
+    f3 np = mean * (float)n + L;
+    float dv = (float)(++n);
+    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+  }
+  F.color[3 * pix] = mean.x;
+  F.color[3 * pix + 1] = mean.y;
+  F.color[3 * pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * pix] = gamma8(mean.x);
+  F.display[3 * pix + 1] = gamma8(mean.y);
+  F.display[3 * pix + 2] = gamma8(mean.z);
+  if (P.spp) {
+    F.normal[3 * pix] = aov.normal.x;
+    F.normal[3 * pix + 1] = aov.normal.y;
+    F.normal[3 * pix + 2] = aov.normal.z;
+    F.depth[pix] = aov.depth;
+    F.material[pix] = aov.id;
+  }
+  if (COUNT) {
+    atomicAdd(&counters->samples, (unsigned long long)P.spp);
+    atomicAdd(&counters->segments, (unsigned long long)segments);
+    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+  }
+}
+
+// ---- multi-GPU packing: 10 words per pixel (colour, count, normal, depth, id)
+constexpr uint32_t kPackWords = 10;
+
+__global__ void pack_tiles(DevFrame F, Launch P, uint32_t owned_max, uint32_t* __restrict__ out) {
+  const uint32_t ts = P.tile_size;
+  size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t total = (size_t)owned_max * ts * ts;
+  if (gid >= total) return;
+  uint32_t k = (uint32_t)(gid / (ts * ts)), in = (uint32_t)(gid % (ts * ts));
+  uint32_t tile = P.tile_offset + k * P.tile_stride;
+  uint32_t* o = out + gid * kPackWords;
+  uint32_t tiles_y = (F.height + ts - 1) / ts;
+  if (tile >= P.tiles_x * tiles_y) {
+    for (uint32_t i = 0; i < kPackWords; i++) o[i] = 0;
+    return;
+  }
+  uint32_t x = (tile % P.tiles_x) * ts + in % ts, y = (tile / P.tiles_x) * ts + in / ts;
+  if (x >= F.width || y >= F.height) {
+    for (uint32_t i = 0; i < kPackWords; i++) o[i] = 0;
+    return;
+  }
+  size_t p = (size_t)y * F.width + x;
+  o[0] = __float_as_uint(F.color[3 * p]);
+  o[1] = __float_as_uint(F.color[3 * p + 1]);
+  o[2] = __float_as_uint(F.color[3 * p + 2]);
+  o[3] = F.count[p];
+  o[4] = __float_as_uint(F.normal[3 * p]);
+  o[5] = __float_as_uint(F.normal[3 * p + 1]);
+  o[6] = __float_as_uint(F.normal[3 * p + 2]);
+  o[7] = __float_as_uint(F.depth[p]);
+  o[8] = (uint32_t)(F.material[p] & 0xFFFFFFFFull);
+  o[9] = (uint32_t)(F.material[p] >> 32);
+}
+
+__global__ void unpack_tiles(DevFrame F, Launch P, uint32_t owned_max, uint32_t nranks, uint32_t self,
+                             const uint32_t* __restrict__ in) {
+  const uint32_t ts = P.tile_size;
+  size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t per_rank = (size_t)owned_max * ts * ts;
+  if (gid >= per_rank * nranks) return;
+  uint32_t rank = (uint32_t)(gid / per_rank);
+  if (rank == self) return;
+  size_t rem = gid % per_rank;
+  uint32_t k = (uint32_t)(rem / (ts * ts)), inpix = (uint32_t)(rem % (ts * ts));
+  uint32_t tile = rank + k * nranks;
+  uint32_t tiles_y = (F.height + ts - 1) / ts;
+  if (tile >= P.tiles_x * tiles_y) return;
+  uint32_t x = (tile % P.tiles_x) * ts + inpix % ts, y = (tile / P.tiles_x) * ts + inpix / ts;
+  if (x >= F.width || y >= F.height) return;
+  size_t p = (size_t)y * F.width + x;
+  const uint32_t* w = in + gid * kPackWords;
+  float c0 = __uint_as_float(w[0]), c1 = __uint_as_float(w[1]), c2 = __uint_as_float(w[2]);
+  F.color[3 * p] = c0;
+  F.color[3 * p + 1] = c1;
+  F.color[3 * p + 2] = c2;
+  F.count[p] = w[3];
+  F.normal[3 * p] = __uint_as_float(w[4]);
+  F.normal[3 * p + 1] = __uint_as_float(w[5]);
+  F.normal[3 * p + 2] = __uint_as_float(w[6]);
+  F.depth[p] = __uint_as_float(w[7]);
+  F.material[p] = (uint64_t)w[8] | ((uint64_t)w[9] << 32);
+  F.display[3 * p] = gamma8(c0);
+  F.display[3 * p + 1] = gamma8(c1);
+  F.display[3 * p + 2] = gamma8(c2);
+}
+
+}  // namespace dev
+}  // namespace fs
+
+// ============================================================================
+// C ABI
+// ============================================================================
+using namespace fs;
+
+namespace {
+
+thread_local std::string g_error;
+
+int fail(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+
+#define FS_HIP(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(FS_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace
+
+struct fs_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool have_scene = false;
+  DevBuf objects, nodes, tris, tri_normals, materials, table, counters, pack_send, pack_recv;
+  DevScene scene{};
+  uint32_t num_objects = 0;
+  PreparedScene host;
+  double upload_ms = 0.0;
+  float last_ms = 0.0f;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+struct fs_frame {
+  fs_context* ctx = nullptr;
+  uint32_t width = 0, height = 0;
+  DevBuf color, count, display, normal, depth, material;
+};
+
+namespace {
+
+int set_device(fs_context* ctx) {
+  FS_HIP(hipSetDevice(ctx->device));
+  return FS_OK;
+}
+
+int upload(fs_context* ctx, DevBuf* b, const void* src, size_t bytes) {
+  b->release();
+  size_t alloc = bytes ? bytes : 16;
+  FS_HIP(hipMalloc(&b->p, alloc));
+  b->bytes = alloc;
+  if (bytes) FS_HIP(hipMemcpyAsync(b->p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return FS_OK;
+}
+
+int ensure(DevBuf* b, size_t bytes) {
+  if (b->bytes >= bytes && b->p) return FS_OK;
+  b->release();
+  FS_HIP(hipMalloc(&b->p, bytes));
+  b->bytes = bytes;
+  return FS_OK;
+}
+
+DevFrame frame_view(fs_frame* f) {
+  DevFrame F;
+  F.color = (float*)f->color.p;
+  F.count = (uint32_t*)f->count.p;
+  F.display = (uint8_t*)f->display.p;
+  F.normal = (float*)f->normal.p;
+  F.depth = (float*)f->depth.p;
+  F.material = (uint64_t*)f->material.p;
+  F.width = f->width;
+  F.height = f->height;
+  return F;
+}
+
+// engine.cpp:170-197, evaluated on the host with the same libm as the oracle.
+DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
+  DevCamera b;
+  b.width = (float)W;
+  b.height = (float)H;
+  float aspect = b.width / b.height;
+  float fovy = (float)((double)(c->fov_y * kPi) / 180.0);
+  float fovx = (float)(2.0 * std::atan(std::tan((double)fovy * 0.5) * (double)aspect));
+  f3 origin = mk3(c->origin[0], c->origin[1], c->origin[2]);
+  f3 target = mk3(c->target[0], c->target[1], c->target[2]);
+  f3 fwd = normalize(target - origin);
+  b.origin = origin;
+  b.right = normalize(cross(mk3(0, 1, 0), fwd));
+  b.up = normalize(cross(fwd, b.right));
+  b.hph = tanf(fovy * 0.5f) * c->z_far;
+  b.hpw = tanf(fovx * 0.5f) * c->z_far;
+  b.proj_origin = origin + fwd * c->z_far;
+  b.focal = plane_np(fwd * -1.0f, origin + fwd * c->focal_depth);
+  b.aperture = c->aperture_size;
+  b.z_far = c->z_far;
+  b.fast_render = c->fast_render;
+  return b;
+}
+
+size_t plane_bytes(int plane, size_t pixels) {
+  switch (plane) {
+    case FS_PLANE_COLOR:
+    case FS_PLANE_NORMAL:
+      return 12 * pixels;
+    case FS_PLANE_COUNT:
+    case FS_PLANE_DEPTH:
+      return 4 * pixels;
+    case FS_PLANE_DISPLAY:
+      return 3 * pixels;
+    case FS_PLANE_MATERIAL:
+      return 8 * pixels;
+    default:
+      return 0;
+  }
+}
+DevBuf* plane_buf(fs_frame* f, int plane) {
+  switch (plane) {
+    case FS_PLANE_COLOR:
+      return &f->color;
+    case FS_PLANE_COUNT:
+      return &f->count;
+    case FS_PLANE_DISPLAY:
+      return &f->display;
+    case FS_PLANE_NORMAL:
+      return &f->normal;
+    case FS_PLANE_DEPTH:
+      return &f->depth;
+    case FS_PLANE_MATERIAL:
+      return &f->material;
+    default:
+      return nullptr;
+  }
+}
+
+int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uint32_t* stride) {
+  if (!p) return fail(FS_ERR_INVALID, "null render params");
+  if (p->width != f->width || p->height != f->height)
+    return fail(FS_ERR_INVALID, "render size does not match the frame");
+  if (p->width < 2 || p->height < 2) return fail(FS_ERR_INVALID, "frame must be at least 2x2 (engine.cpp:214)");
+  *ts = p->tile_size ? p->tile_size : 64;
+  *stride = p->tile_stride ? p->tile_stride : 1;
+  if (*ts % 8 || *ts > 1024) return fail(FS_ERR_INVALID, "tile_size must be a multiple of 8, <= 1024");
+  if (p->tile_offset >= *stride) return fail(FS_ERR_INVALID, "tile_offset must be < tile_stride");
+  if ((uint64_t)p->sample_base + p->spp > (1ull << 20))
+    return fail(FS_ERR_INVALID, "sample index must stay below 2^20 (seed layout)");
+  return FS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fs_abi_version(void) { return FS_ABI_VERSION; }
+const char* fs_last_error(void) { return g_error.c_str(); }
+
+int fs_device_count(int* count) {
+  if (!count) return fail(FS_ERR_INVALID, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return FS_OK;
+}
+
+int fs_create(int device, fs_context** out) {
+  if (!out) return fail(FS_ERR_INVALID, "null out");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(FS_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) return fail(FS_ERR_INVALID, "device index out of range");
+  std::unique_ptr<fs_context> ctx(new fs_context());
+  ctx->device = device;
+  FS_HIP(hipSetDevice(device));
+  FS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  FS_HIP(hipEventCreate(&ctx->ev0));
+  FS_HIP(hipEventCreate(&ctx->ev1));
+  FS_HIP(hipMalloc(&ctx->counters.p, sizeof(DevCounters)));
+  ctx->counters.bytes = sizeof(DevCounters);
+  FS_HIP(hipMemset(ctx->counters.p, 0, sizeof(DevCounters)));
+  *out = ctx.release();
+  return FS_OK;
+}
+
+int fs_destroy(fs_context* ctx) {
+  if (!ctx) return FS_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->materials, &ctx->table,
+                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
+    b->release();
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return FS_OK;
+}
+
+int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
+  if (!ctx) return fail(FS_ERR_INVALID, "null context");
+  std::string err;
+  PreparedScene P;
+  int rc = prepare_scene(desc, &P, &err);
+  if (rc) return fail(rc, err);
+  if (P.materials.size() > 255) return fail(FS_ERR_INVALID, "at most 255 materials are supported");
+  if ((rc = set_device(ctx))) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  ctx->have_scene = false;
+  if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
+  if ((rc = upload(ctx, &ctx->nodes, P.nodes.data(), P.nodes.size() * sizeof(BvhNode)))) return rc;
+  if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri)))) return rc;
+  if ((rc = upload(ctx, &ctx->tri_normals, P.tri_normals.data(), P.tri_normals.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
+  if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  DevScene& S = ctx->scene;
+  S.objects = (const DevObject*)ctx->objects.p;
+  S.nodes = (const BvhNode*)ctx->nodes.p;
+  S.tris = (const DevTri*)ctx->tris.p;
+  S.tri_normals = (const float4*)ctx->tri_normals.p;
+  S.materials = (const fs_material*)ctx->materials.p;
+  S.table = (const float4*)ctx->table.p;
+  S.num_objects = (uint32_t)P.objects.size();
+  S.sky = P.sky;
+  // Scene::SampleSky (scene.cpp:157-162): LightMaterial emissive x 3; a
+  // non-Light sky dispatches to its own Sample with black light (0, or the
+  // glow term of a GlowMaterial) — scene.cpp:383 static_pointer_cast.
+  const fs_material& sky = P.materials[P.sky];
+  f3 sv = mk3(0, 0, 0);
+  if (sky.kind == FS_MAT_LIGHT) sv = mk3(sky.emissive[0], sky.emissive[1], sky.emissive[2]);
+  if (sky.kind == FS_MAT_GLOW) sv = mk3(sky.glow[0], sky.glow[1], sky.glow[2]);
+  sv = sv * (float)3.0;
+  S.sky_r = sv.x;
+  S.sky_g = sv.y;
+  S.sky_b = sv.z;
+  S.sky_id = sky.id;
+  ctx->num_objects = S.num_objects;
+  ctx->host = std::move(P);
+  ctx->have_scene = true;
+  return FS_OK;
+}
+
+int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms, uint64_t* num_triangles,
+                   uint64_t* num_nodes, uint64_t* device_bytes) {
+  if (!ctx) return fail(FS_ERR_INVALID, "null context");
+  if (!ctx->have_scene) return fail(FS_ERR_STATE, "no scene uploaded");
+  if (build_ms) *build_ms = ctx->host.build_ms;
+  if (upload_ms) *upload_ms = ctx->upload_ms;
+  if (num_triangles) *num_triangles = ctx->host.tris.size();
+  if (num_nodes) *num_nodes = ctx->host.nodes.size();
+  if (device_bytes)
+    *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
+                     ctx->materials.bytes + ctx->table.bytes;
+  return FS_OK;
+}
+
+int fs_frame_create(fs_context* ctx, uint32_t width, uint32_t height, fs_frame** out) {
+  if (!ctx || !out) return fail(FS_ERR_INVALID, "null argument");
+  if (width == 0 || height == 0) return fail(FS_ERR_INVALID, "empty frame");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  std::unique_ptr<fs_frame> f(new fs_frame());
+  f->ctx = ctx;
+  f->width = width;
+  f->height = height;
+  size_t px = (size_t)width * height;
+  for (int pl = FS_PLANE_COLOR; pl <= FS_PLANE_MATERIAL; pl++) {
+    DevBuf* b = plane_buf(f.get(), pl);
+    FS_HIP(hipMalloc(&b->p, plane_bytes(pl, px)));
+    b->bytes = plane_bytes(pl, px);
+  }
+  fs_frame* raw = f.release();
+  rc = fs_frame_reset(raw);
+  if (rc) {
+    fs_frame_destroy(raw);
+    return rc;
+  }
+  *out = raw;
+  return FS_OK;
+}
+
+int fs_frame_destroy(fs_frame* f) {
+  if (!f) return FS_OK;
+  (void)hipSetDevice(f->ctx->device);
+  (void)hipStreamSynchronize(f->ctx->stream);
+  for (int pl = FS_PLANE_COLOR; pl <= FS_PLANE_MATERIAL; pl++) plane_buf(f, pl)->release();
+  delete f;
+  return FS_OK;
+}
+
+int fs_frame_reset(fs_frame* f) {  // DisplayFrame::Reset (frame.cpp:43-51)
+  if (!f) return fail(FS_ERR_INVALID, "null frame");
+  int rc;
+  if ((rc = set_device(f->ctx))) return rc;
+  for (int pl = FS_PLANE_COLOR; pl <= FS_PLANE_MATERIAL; pl++) {
+    DevBuf* b = plane_buf(f, pl);
+    FS_HIP(hipMemsetAsync(b->p, 0, b->bytes, f->ctx->stream));
+  }
+  FS_HIP(hipStreamSynchronize(f->ctx->stream));
+  return FS_OK;
+}
+
+int fs_frame_read(fs_frame* f, int plane, void* dst, size_t bytes) {
+  if (!f || !dst) return fail(FS_ERR_INVALID, "null argument");
+  DevBuf* b = plane_buf(f, plane);
+  if (!b) return fail(FS_ERR_INVALID, "unknown plane");
+  if (bytes != b->bytes) return fail(FS_ERR_INVALID, "byte count does not match the plane size");
+  int rc;
+  if ((rc = set_device(f->ctx))) return rc;
+  FS_HIP(hipMemcpyAsync(dst, b->p, bytes, hipMemcpyDeviceToHost, f->ctx->stream));
+  FS_HIP(hipStreamSynchronize(f->ctx->stream));
+  return FS_OK;
+}
+
+int fs_frame_write(fs_frame* f, int plane, const void* src, size_t bytes) {
+  if (!f || !src) return fail(FS_ERR_INVALID, "null argument");
+  DevBuf* b = plane_buf(f, plane);
+  if (!b) return fail(FS_ERR_INVALID, "unknown plane");
+  if (bytes != b->bytes) return fail(FS_ERR_INVALID, "byte count does not match the plane size");
+  int rc;
+  if ((rc = set_device(f->ctx))) return rc;
+  FS_HIP(hipMemcpyAsync(b->p, src, bytes, hipMemcpyHostToDevice, f->ctx->stream));
+  FS_HIP(hipStreamSynchronize(f->ctx->stream));
+  return FS_OK;
+}
+
+int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* params, fs_frame* frame) {
+  if (!ctx || !camera || !params || !frame) return fail(FS_ERR_INVALID, "null argument");
+  if (!ctx->have_scene) return fail(FS_ERR_STATE, "fs_render before fs_upload_scene");
+  if (frame->ctx != ctx) return fail(FS_ERR_INVALID, "frame belongs to another context");
+  uint32_t ts, stride;
+  int rc = check_params(params, frame, &ts, &stride);
+  if (rc) return rc;
+  if ((rc = set_device(ctx))) return rc;
+  Launch L;
+  L.tile_size = ts;
+  L.tiles_x = (params->width + ts - 1) / ts;
+  uint32_t tiles_y = (params->height + ts - 1) / ts;
+  uint32_t tiles = L.tiles_x * tiles_y;
+  L.tile_offset = params->tile_offset;
+  L.tile_stride = stride;
+  L.seed = params->seed;
+  uint32_t owned = params->tile_offset < tiles ? (tiles - params->tile_offset + stride - 1) / stride : 0;
+  uint64_t blocks = (uint64_t)owned * (ts / 8) * (ts / 8);
+  DevCamera C = camera_basis(camera, params->width, params->height);
+  DevFrame F = frame_view(frame);
+  bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
+  // Long renders are split into launches of at most `chunk` samples per
+  // pixel; the running mean lives in the frame, so the result is identical.
+  const uint32_t chunk = 32;
+  FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+  for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
+    L.sample_base = params->sample_base + done;
+    L.spp = std::min(chunk, params->spp - done);
+    if (count)
+      hipLaunchKernelGGL(dev::render_kernel<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream,
+                         ctx->scene, C, F, L, (DevCounters*)ctx->counters.p);
+    else
+      hipLaunchKernelGGL(dev::render_kernel<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream,
+                         ctx->scene, C, F, L, (DevCounters*)ctx->counters.p);
+    FS_HIP(hipGetLastError());
+  }
+  FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+  return FS_OK;
+}
+
+int fs_synchronize(fs_context* ctx) {
+  if (!ctx) return fail(FS_ERR_INVALID, "null context");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  return FS_OK;
+}
+
+int fs_last_render_ms(fs_context* ctx, float* ms) {
+  if (!ctx || !ms) return fail(FS_ERR_INVALID, "null argument");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  FS_HIP(hipEventSynchronize(ctx->ev1));
+  FS_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+  return FS_OK;
+}
+
+int fs_read_counters(fs_context* ctx, fs_counters* out) {
+  if (!ctx || !out) return fail(FS_ERR_INVALID, "null argument");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  DevCounters c;
+  FS_HIP(hipMemcpyAsync(&c, ctx->counters.p, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
+  FS_HIP(hipMemsetAsync(ctx->counters.p, 0, sizeof(c), ctx->stream));
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  out->samples = c.samples;
+  out->segments = c.segments;
+  out->node_visits = c.node_visits;
+  out->tri_tests = c.tri_tests;
+  out->prim_tests = c.prim_tests;
+  return FS_OK;
+}
+
+// ---- RCCL ---------------------------------------------------------------
+int fs_comm_unique_id(uint8_t id[FS_COMM_ID_BYTES]) {
+  if (!id) return fail(FS_ERR_INVALID, "null id");
+  static_assert(sizeof(ncclUniqueId) == FS_COMM_ID_BYTES, "unique id size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id, &u, sizeof(u));
+  return FS_OK;
+}
+
+int fs_comm_init(fs_context* ctx, int nranks, int rank, const uint8_t id[FS_COMM_ID_BYTES]) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(FS_ERR_INVALID, "bad comm arguments");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  ctx->comm = nullptr;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+  if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return FS_OK;
+}
+
+int fs_comm_destroy(fs_context* ctx) {
+  if (!ctx) return fail(FS_ERR_INVALID, "null context");
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  ctx->comm = nullptr;
+  ctx->nranks = 1;
+  ctx->rank = 0;
+  return FS_OK;
+}
+
+// Packs this rank's owned tiles, ncclGather's them to root over xGMI and
+// scatters them into root's frame. One collective per render.
+int fs_frame_gather(fs_context* ctx, fs_frame* frame, const fs_render_params* params, int root) {
+  if (!ctx || !frame || !params) return fail(FS_ERR_INVALID, "null argument");
+  if (!ctx->comm) return fail(FS_ERR_STATE, "fs_frame_gather before fs_comm_init");
+  uint32_t ts, stride;
+  int rc = check_params(params, frame, &ts, &stride);
+  if (rc) return rc;
+  if ((int)stride != ctx->nranks || (int)params->tile_offset != ctx->rank)
+    return fail(FS_ERR_INVALID, "tiling must be tile_offset=rank, tile_stride=nranks");
+  if (root < 0 || root >= ctx->nranks) return fail(FS_ERR_INVALID, "root out of range");
+  if ((rc = set_device(ctx))) return rc;
+  Launch L{};
+  L.tile_size = ts;
+  L.tiles_x = (params->width + ts - 1) / ts;
+  L.tile_offset = params->tile_offset;
+  L.tile_stride = stride;
+  uint32_t tiles = L.tiles_x * ((params->height + ts - 1) / ts);
+  uint32_t owned_max = (tiles + stride - 1) / stride;
+  size_t per_rank_words = (size_t)owned_max * ts * ts * dev::kPackWords;
+  if ((rc = ensure(&ctx->pack_send, per_rank_words * 4))) return rc;
+  if (ctx->rank == root && (rc = ensure(&ctx->pack_recv, per_rank_words * 4 * ctx->nranks))) return rc;
+  DevFrame F = frame_view(frame);
+  size_t n = (size_t)owned_max * ts * ts;
+  hipLaunchKernelGGL(dev::pack_tiles, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, ctx->stream, F, L, owned_max,
+                     (uint32_t*)ctx->pack_send.p);
+  FS_HIP(hipGetLastError());
+  ncclResult_t r = ncclGather(ctx->pack_send.p, ctx->rank == root ? ctx->pack_recv.p : nullptr, per_rank_words,
+                              ncclUint32, root, ctx->comm, ctx->stream);
+  if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
+  if (ctx->rank == root) {
+    size_t total = n * ctx->nranks;
+    hipLaunchKernelGGL(dev::unpack_tiles, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, ctx->stream, F, L,
+                       owned_max, (uint32_t)ctx->nranks, (uint32_t)ctx->rank, (const uint32_t*)ctx->pack_recv.p);
+    FS_HIP(hipGetLastError());
+  }
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  return FS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// fs_kernels.h — device code of the hot path (one wave64 per 8x8 pixel block).
+//
+// Restates, per sample, engine.cpp:59-251 (ray generation, TraceStep),
+// scene.cpp:227-249 (closest hit + back-face flip), object.cpp / intersect.cpp
+// (primitive tests), material.cpp + normal.cpp (BRDF sampling and shading)
+// and frame.cpp:53-85 (running-mean accumulation). The recursion of TraceStep
+// is unrolled into a forward pass that stages each bounce's shading scalars
+// in LDS and a backward pass that applies Material::Sample in the reference's
+// order, so the float rounding matches the recursive reference bit for bit.
+#pragma once
+
+#include "fs_scene.h"
+
+namespace fs {
+
+constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS columns
+
+struct DevScene {
+  const DevObject* __restrict__ objects;
+  const BvhNode* __restrict__ nodes;
+  const DevTri* __restrict__ tris;
+  const float4* __restrict__ tri_normals;
+  const fs_material* __restrict__ materials;
+  const float4* __restrict__ table;
+  uint32_t num_objects;
+  int32_t sky;
+  float sky_r, sky_g, sky_b;  // Scene::SampleSky value (scene.cpp:157-162), x3 applied
+  uint32_t sky_id;
+};
+
+// Camera basis computed on the host exactly as engine.cpp:170-197.
+struct DevCamera {
+  f3 origin, right, up, proj_origin;
+  float hpw, hph, width, height;
+  float aperture, z_far;
+  f4 focal;
+  int32_t fast_render;
+};
+
+struct DevFrame {
+  float* color;
+  uint32_t* count;
+  uint8_t* display;
+  float* normal;
+  float* depth;
+  uint64_t* material;
+  uint32_t width, height;
+};
+
+struct DevCounters {
+  unsigned long long samples, segments, node_visits, tri_tests, prim_tests;
+};
+
+struct Launch {
+  uint32_t tile_size, tiles_x, tile_offset, tile_stride;
+  uint32_t sample_base, spp;
+  uint64_t seed;
+};
+
+}  // namespace fs

@@ -1,0 +1,580 @@
+// fs_scene.cpp — host preparation of the device scene.
+//
+// 1. Restates the reference object constructors (object.cpp, volume.cpp,
+//    mesh.cpp:168-275) so the device sees exactly the planes, tangents and
+//    baked vertices the reference would hold.
+// 2. Replaces the reference's per-mesh 8-ary octree (mesh.cpp:39-152,
+//    bvh.h) with a binned-SAH BVH2 per mesh. Only the acceleration structure
+//    changes: the leaf test is the reference's ray_intersect_triangle, and the
+//    traversal keeps the reference's closest-hit rule (strict '<', the first
+//    object in list order wins ties). Boxes are padded so culling is
+//    conservative. See DESIGN.md §"Acceleration structure".
+#include "fs_scene.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+namespace fs {
+namespace {
+
+// ---- matrix4 (math/matrix4.h, column-major) -------------------------------
+struct M4 {
+  float m[16];
+};
+M4 m4_identity() {  // matrix4.h:240-246
+  M4 r;
+  std::memset(&r, 0, sizeof(r));
+  r.m[0] = r.m[5] = r.m[10] = r.m[15] = 1;
+  return r;
+}
+M4 m4_mul(const M4& a, const M4& b) {  // matrix4.h:529-546
+  M4 o;
+  for (int k = 0; k < 16; k++) {
+    int r = k % 4, c = k / 4;
+    o.m[k] = 0.0f;
+    for (int i = 0; i < 4; i++) o.m[k] += a.m[r + (i * 4)] * b.m[(c * 4) + i];
+  }
+  return o;
+}
+M4 m4_rotation(float rad, f3 axis) {  // matrix4.h:270-301
+  float c = std::cos(rad), s = std::sin(rad), t = 1.0f - c;
+  f3 a = normalize(axis);
+  float x = a.x, y = a.y, z = a.z;
+  M4 o;
+  o.m[0] = t * x * x + c;
+  o.m[4] = t * x * y - s * z;
+  o.m[8] = t * x * z + s * y;
+  o.m[12] = 0.0f;
+  o.m[1] = t * x * y + s * z;
+  o.m[5] = t * y * y + c;
+  o.m[9] = t * y * z - s * x;
+  o.m[13] = 0.0f;
+  o.m[2] = t * x * z - s * y;
+  o.m[6] = t * y * z + s * x;
+  o.m[10] = t * z * z + c;
+  o.m[14] = 0.0f;
+  o.m[3] = 0.0f;
+  o.m[7] = 0.0f;
+  o.m[11] = 0.0f;
+  o.m[15] = 1.0f;
+  return o;
+}
+f3 m4_apply(const M4& M, f3 v) {  // matrix4.h:552-557 with w = 1
+  const float* m = M.m;
+  const float w = 1.0f;
+  return mk3(v.x * m[0] + v.y * m[4] + v.z * m[8] + w * m[12],
+             v.x * m[1] + v.y * m[5] + v.z * m[9] + w * m[13],
+             v.x * m[2] + v.y * m[6] + v.z * m[10] + w * m[14]);
+}
+
+// bounds (volume.cpp:162-191): first point initialises min and max.
+struct Bounds {
+  f3 mn{0, 0, 0}, mx{0, 0, 0};
+  uint32_t count = 0;
+  void add(f3 p) {
+    if (count == 0) {
+      mn = mx = p;
+      count = 1;
+      return;
+    }
+    count++;
+    if (p.x > mx.x) mx.x = p.x;
+    if (p.y > mx.y) mx.y = p.y;
+    if (p.z > mx.z) mx.z = p.z;
+    if (p.x < mn.x) mn.x = p.x;
+    if (p.y < mn.y) mn.y = p.y;
+    if (p.z < mn.z) mn.z = p.z;
+  }
+  f3 center() const { return (mn + mx) * 0.5f; }
+};
+
+// ---- BVH builder ------------------------------------------------------------
+struct Box {
+  float lo[3] = {INFINITY, INFINITY, INFINITY};
+  float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const float* p) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  bool empty() const { return lo[0] > hi[0]; }
+  float area() const {
+    if (empty()) return 0.0f;
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Prim {
+  Box box;
+  float c[3];
+  uint32_t face;
+};
+
+constexpr int kBins = 16;
+constexpr uint32_t kLeafTarget = 4;
+
+class BvhBuilder {
+ public:
+  BvhBuilder(std::vector<BvhNode>* nodes, std::vector<DevTri>* tris, std::vector<float>* tri_normals,
+             const std::vector<DevTri>* mesh_tris, const std::vector<float>* mesh_normals)
+      : nodes_(nodes), tris_(tris), tri_normals_(tri_normals), mesh_tris_(mesh_tris), mesh_normals_(mesh_normals) {}
+
+  // Builds the tree over all faces; returns the root node index.
+  uint32_t build(std::vector<Prim>& prims, uint32_t* max_depth) {
+    prims_ = &prims;
+    uint32_t root = alloc_node();
+    Box all = range_box(0, (uint32_t)prims.size());
+    if (prims.size() <= kLeafTarget) {
+      set_child(root, 0, all, make_leaf(0, (uint32_t)prims.size()));
+      set_child(root, 1, Box(), kLeafBit);  // empty
+    } else {
+      split_into(root, 0, (uint32_t)prims.size(), 1);
+    }
+    *max_depth = std::max(*max_depth, max_depth_);
+    return root;
+  }
+
+ private:
+  uint32_t alloc_node() {
+    BvhNode n;
+    std::memset(&n, 0, sizeof(n));
+    nodes_->push_back(n);
+    return (uint32_t)nodes_->size() - 1;
+  }
+  Box range_box(uint32_t b, uint32_t e) const {
+    Box r;
+    for (uint32_t i = b; i < e; i++) r.grow((*prims_)[i].box);
+    return r;
+  }
+  // Conservative padding: the reference triangle test may accept a hit point
+  // a few ulps outside the exact triangle, so boxes are widened.
+  static void pad(Box* b) {
+    if (b->empty()) return;
+    float s = 1.0f;
+    for (int k = 0; k < 3; k++) s = std::max(s, std::max(std::fabs(b->lo[k]), std::fabs(b->hi[k])));
+    float p = 4e-5f * s;
+    for (int k = 0; k < 3; k++) {
+      b->lo[k] -= p;
+      b->hi[k] += p;
+    }
+  }
+  void set_child(uint32_t node, int slot, Box b, uint32_t word) {
+    pad(&b);
+    BvhNode& n = (*nodes_)[node];
+    if (b.empty()) {  // a far-away point box: never intersected by a segment of the scene
+      n.lo_x[slot] = n.lo_y[slot] = n.lo_z[slot] = 3e30f;
+      n.hi_x[slot] = n.hi_y[slot] = n.hi_z[slot] = 3e30f;
+    } else {
+      n.lo_x[slot] = b.lo[0];
+      n.lo_y[slot] = b.lo[1];
+      n.lo_z[slot] = b.lo[2];
+      n.hi_x[slot] = b.hi[0];
+      n.hi_y[slot] = b.hi[1];
+      n.hi_z[slot] = b.hi[2];
+    }
+    n.child[slot] = word;
+  }
+  uint32_t make_leaf(uint32_t b, uint32_t e) {
+    uint32_t start = (uint32_t)tris_->size();
+    for (uint32_t i = b; i < e; i++) {
+      uint32_t f = (*prims_)[i].face;
+      tris_->push_back((*mesh_tris_)[f]);
+      if (!mesh_normals_->empty())
+        tri_normals_->insert(tri_normals_->end(), mesh_normals_->begin() + 12 * (size_t)f,
+                             mesh_normals_->begin() + 12 * (size_t)f + 12);
+    }
+    return kLeafBit | ((e - b) << 24) | start;
+  }
+  // Partitions [b,e) into two halves; returns the split index.
+  uint32_t partition(uint32_t b, uint32_t e, uint32_t depth) {
+    std::vector<Prim>& P = *prims_;
+    uint32_t n = e - b;
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = b; i < e; i++)
+      for (int k = 0; k < 3; k++) {
+        cmin[k] = std::min(cmin[k], P[i].c[k]);
+        cmax[k] = std::max(cmax[k], P[i].c[k]);
+      }
+    int axis = 0;
+    for (int k = 1; k < 3; k++)
+      if (cmax[k] - cmin[k] > cmax[axis] - cmin[axis]) axis = k;
+    // Depth guard: fall back to an object median near the stack bound.
+    uint32_t need = 0;
+    for (uint32_t m = n; m > kLeafTarget; m = (m + 1) / 2) need++;
+    bool median = depth + need + 1 >= kTraversalStack - 1 || cmax[axis] <= cmin[axis];
+    if (!median) {
+      float best_cost = INFINITY;
+      int best_axis = -1, best_bin = -1;
+      for (int ax = 0; ax < 3; ax++) {
+        float ext = cmax[ax] - cmin[ax];
+        if (!(ext > 0.0f)) continue;
+        Box bb[kBins];
+        uint32_t bc[kBins] = {0};
+        float scale = kBins / ext;
+        for (uint32_t i = b; i < e; i++) {
+          int k = std::min(kBins - 1, (int)((P[i].c[ax] - cmin[ax]) * scale));
+          bb[k].grow(P[i].box);
+          bc[k]++;
+        }
+        Box left[kBins];
+        uint32_t lc[kBins];
+        Box acc;
+        uint32_t cnt = 0;
+        for (int k = 0; k < kBins; k++) {
+          acc.grow(bb[k]);
+          cnt += bc[k];
+          left[k] = acc;
+          lc[k] = cnt;
+        }
+        Box racc;
+        uint32_t rcnt = 0;
+        for (int k = kBins - 1; k > 0; k--) {
+          racc.grow(bb[k]);
+          rcnt += bc[k];
+          if (lc[k - 1] == 0 || rcnt == 0) continue;
+          float cost = left[k - 1].area() * lc[k - 1] + racc.area() * rcnt;
+          if (cost < best_cost) {
+            best_cost = cost;
+            best_axis = ax;
+            best_bin = k;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        float ext = cmax[best_axis] - cmin[best_axis];
+        float scale = kBins / ext;
+        auto mid = std::partition(P.begin() + b, P.begin() + e, [&](const Prim& p) {
+          int k = std::min(kBins - 1, (int)((p.c[best_axis] - cmin[best_axis]) * scale));
+          return k < best_bin;
+        });
+        uint32_t m = (uint32_t)(mid - P.begin());
+        if (m > b && m < e) return m;
+      }
+    }
+    uint32_t m = b + n / 2;
+    std::nth_element(P.begin() + b, P.begin() + m, P.begin() + e,
+                     [&](const Prim& x, const Prim& y) { return x.c[axis] < y.c[axis]; });
+    return m;
+  }
+  // Builds the two children of `node` over [b,e).
+  void split_into(uint32_t node, uint32_t b, uint32_t e, uint32_t depth) {
+    max_depth_ = std::max(max_depth_, depth);
+    uint32_t m = partition(b, e, depth);
+    uint32_t ranges[2][2] = {{b, m}, {m, e}};
+    for (int s = 0; s < 2; s++) {
+      uint32_t cb = ranges[s][0], ce = ranges[s][1];
+      Box cbox = range_box(cb, ce);
+      if (ce - cb <= kLeafTarget || depth + 1 >= kTraversalStack - 1) {
+        set_child(node, s, cbox, make_leaf(cb, ce));
+      } else {
+        uint32_t c = alloc_node();
+        set_child(node, s, cbox, c);
+        split_into(c, cb, ce, depth + 1);
+      }
+    }
+  }
+
+  std::vector<BvhNode>* nodes_;
+  std::vector<DevTri>* tris_;
+  std::vector<float>* tri_normals_;
+  const std::vector<DevTri>* mesh_tris_;
+  const std::vector<float>* mesh_normals_;
+  std::vector<Prim>* prims_ = nullptr;
+  uint32_t max_depth_ = 0;
+};
+
+void cube_planes(const f3* v, float* d) {  // volume.cpp:234-247
+  f4 p[6] = {plane_3p(v[0], v[1], v[2]), plane_3p(v[6], v[5], v[4]), plane_3p(v[5], v[6], v[2]),
+             plane_3p(v[7], v[4], v[0]), plane_3p(v[4], v[5], v[1]), plane_3p(v[6], v[7], v[3])};
+  for (int i = 0; i < 6; i++) {
+    d[4 * i + 0] = p[i].x;
+    d[4 * i + 1] = p[i].y;
+    d[4 * i + 2] = p[i].z;
+    d[4 * i + 3] = p[i].w;
+  }
+}
+
+void put3(float* d, f3 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+}
+void put4(float* d, f4 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+  d[3] = v.w;
+}
+
+// Builds one analytic object (object.cpp constructors).
+int build_object(const fs_object& o, DevObject* out, std::string* err) {
+  std::memset(out, 0, sizeof(*out));
+  out->kind = o.kind;
+  out->mat = o.material;
+  const float* a = o.a;
+  switch (o.kind) {
+    case FS_OBJ_SPHERE:  // object.cpp:17-21
+      out->d[0] = a[0];
+      out->d[1] = a[1];
+      out->d[2] = a[2];
+      out->d[3] = a[3];
+      return FS_OK;
+    case FS_OBJ_PLANE:  // object.cpp:38
+      for (int i = 0; i < 4; i++) out->d[i] = a[i];
+      return FS_OK;
+    case FS_OBJ_DISC: {  // object.cpp:75-95 (normal used as given)
+      f3 org = mk3(a[0], a[1], a[2]);
+      put4(out->d, plane_np(mk3(a[3], a[4], a[5]), org));
+      put3(out->d + 4, org);
+      out->d[7] = a[6];
+      return FS_OK;
+    }
+    case FS_OBJ_CUBOID: {  // object.cpp:115-124, volume.cpp:262-283, 434-445
+      f3 org = mk3(a[0], a[1], a[2]);
+      f3 half = mk3((float)(a[3] * 0.5), (float)(a[4] * 0.5), (float)(a[5] * 0.5));
+      Bounds bb;
+      bb.add(org - half);
+      bb.add(org + half);
+      f3 lo = bb.mn, hi = bb.mx;
+      f3 v[8] = {lo,
+                 mk3(hi.x, lo.y, lo.z),
+                 mk3(hi.x, lo.y, hi.z),
+                 mk3(lo.x, lo.y, hi.z),
+                 mk3(lo.x, hi.y, lo.z),
+                 mk3(hi.x, hi.y, lo.z),
+                 mk3(hi.x, hi.y, hi.z),
+                 mk3(lo.x, hi.y, hi.z)};
+      if (o.rotate) {
+        f3 axis = mk3(a[6], a[7], a[8]);
+        float c = (float)std::cos(a[9]), s = (float)std::sin(a[9]);
+        f3 center = bb.center();
+        for (int i = 0; i < 8; i++) v[i] = rotate(v[i] - center, c, s, axis) + center;
+      }
+      cube_planes(v, out->d);
+      return FS_OK;
+    }
+    case FS_OBJ_QUAD_ONWH: {  // object.cpp:167-189
+      f3 nrm = normalize(mk3(a[3], a[4], a[5]));
+      f3 org = mk3(a[0], a[1], a[2]);
+      out->kind = FS_OBJ_QUAD_ONWH;
+      put4(out->d, plane_np(nrm, org));
+      put3(out->d + 4, org);
+      out->d[7] = (float)(a[6] * 0.5);
+      out->d[8] = (float)(a[7] * 0.5);
+      f3 bt = cross(nrm, mk3(0, 1, 0));
+      put3(out->d + 9, bt);
+      put3(out->d + 12, cross(nrm, bt));
+      return FS_OK;
+    }
+    case FS_OBJ_QUAD_PUV: {  // object.cpp:191-211
+      f3 pos = mk3(a[0], a[1], a[2]), u = mk3(a[3], a[4], a[5]), v = mk3(a[6], a[7], a[8]);
+      f3 nrm = normalize(cross(u, v));
+      out->kind = FS_OBJ_QUAD_ONWH;
+      put4(out->d, plane_np(nrm, pos));
+      put3(out->d + 4, pos + u * (float)0.5 + v * (float)0.5);
+      out->d[7] = (float)(length(u) * 0.5);
+      out->d[8] = (float)(length(v) * 0.5);
+      put3(out->d + 9, normalize(u));
+      put3(out->d + 12, normalize(v));
+      return FS_OK;
+    }
+    default:
+      *err = "unknown object kind " + std::to_string(o.kind);
+      return FS_ERR_INVALID;
+  }
+}
+
+}  // namespace
+
+int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!d || !out) {
+    *err = "null scene";
+    return FS_ERR_INVALID;
+  }
+  if (!d->materials || d->num_materials == 0 || !d->normal_table) {
+    *err = "scene needs materials and a normal table (InitializeMaterials)";
+    return FS_ERR_INVALID;
+  }
+  if (d->sky_material < 0 || (uint32_t)d->sky_material >= d->num_materials) {
+    *err = "sky_material out of range";
+    return FS_ERR_INVALID;
+  }
+  if (d->num_objects && !d->objects) {
+    *err = "objects pointer is null";
+    return FS_ERR_INVALID;
+  }
+  PreparedScene& S = *out;
+  S = PreparedScene();
+  S.sky = d->sky_material;
+  S.materials.assign(d->materials, d->materials + d->num_materials);
+  for (const fs_material& m : S.materials) {
+    if (m.kind < FS_MAT_DIFFUSE || m.kind > FS_MAT_FOG) {
+      *err = "unknown material kind " + std::to_string(m.kind);
+      return FS_ERR_INVALID;
+    }
+    if (m.texture >= 0) {
+      *err = "textured materials are not supported by the GPU path yet";
+      return FS_ERR_INVALID;
+    }
+  }
+  S.table.resize(4 * (size_t)FS_NORMAL_TABLE_SIZE);
+  for (uint32_t i = 0; i < FS_NORMAL_TABLE_SIZE; i++) {
+    S.table[4 * i + 0] = d->normal_table[3 * i + 0];
+    S.table[4 * i + 1] = d->normal_table[3 * i + 1];
+    S.table[4 * i + 2] = d->normal_table[3 * i + 2];
+    S.table[4 * i + 3] = 0.0f;
+  }
+
+  // Meshes: MeshObject::MeshObject + BuildBvh face planes.
+  struct MeshOut {
+    uint32_t root = 0;
+    bool tree = false;
+    bool normals = false;
+    Bounds rb;
+  };
+  std::vector<MeshOut> mesh_out(d->num_meshes);
+  bool any_normals = false;
+  for (uint32_t mi = 0; mi < d->num_meshes; mi++)
+    if (d->meshes[mi].normals && d->meshes[mi].num_normals) any_normals = true;
+  for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
+    const fs_mesh& m = d->meshes[mi];
+    if (m.num_triangles && (!m.corners || !m.positions)) {
+      *err = "mesh " + std::to_string(mi) + " has triangles but no positions/corners";
+      return FS_ERR_INVALID;
+    }
+    bool need = false;
+    M4 T = m4_identity(), Sc = m4_identity(), R = m4_identity();
+    if (m.translation[0] || m.translation[1] || m.translation[2]) {
+      need = true;
+      T.m[12] = m.translation[0];
+      T.m[13] = m.translation[1];
+      T.m[14] = m.translation[2];
+    }
+    if (m.scale[0] || m.scale[1] || m.scale[2]) {
+      need = true;
+      Sc.m[0] = m.scale[0];
+      Sc.m[5] = m.scale[1];
+      Sc.m[10] = m.scale[2];
+    }
+    if (m.rotation[0] || m.rotation[1] || m.rotation[2]) {
+      need = true;
+      R = m4_rotation(m.rotation[3], mk3(m.rotation[0], m.rotation[1], m.rotation[2]));
+    }
+    std::vector<f3> verts;
+    if (need) {  // vertices_ is only filled when a transform is needed (mesh.cpp:211-221)
+      M4 M = m4_mul(m4_mul(T, R), Sc);
+      verts.resize(m.num_positions);
+      for (uint32_t i = 0; i < m.num_positions; i++) {
+        f3 v = m4_apply(M, mk3(m.positions[3 * i], m.positions[3 * i + 1], m.positions[3 * i + 2]));
+        verts[i] = v;
+        mesh_out[mi].rb.add(v);
+      }
+    }
+    uint32_t nn = (m.normals ? m.num_normals : 0);
+    std::vector<f3> normals(nn);
+    for (uint32_t i = 0; i < nn; i++) {  // mesh.cpp:223-234
+      f3 n = normalize(mk3(m.normals[3 * i], m.normals[3 * i + 1], m.normals[3 * i + 2]));
+      if (m.invert_normals) n = n * (float)-1.0;
+      normals[i] = n;
+    }
+    mesh_out[mi].normals = nn > 0;
+    uint32_t nt = m.texcoords ? m.num_texcoords : 0;
+    std::vector<DevTri> mtris(m.num_triangles);
+    std::vector<float> mnormals;
+    if (any_normals) mnormals.assign(12 * (size_t)m.num_triangles, 0.0f);
+    for (uint32_t f = 0; f < m.num_triangles; f++) {
+      const int32_t* c = m.corners + 9 * (size_t)f;
+      uint32_t vi[3], ni[3], ti[3];
+      for (int k = 0; k < 3; k++) {  // winding reversed (mesh.cpp:250-260)
+        vi[k] = (uint32_t)c[3 * (2 - k) + 0];
+        ni[k] = (uint32_t)c[3 * (2 - k) + 1];
+        ti[k] = (uint32_t)c[3 * (2 - k) + 2];
+        if (vi[k] >= m.num_positions) {
+          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": vertex index out of range";
+          return FS_ERR_INVALID;
+        }
+        if (nn && ni[k] >= nn) {  // normals_.at() would throw (mesh.cpp:292)
+          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": normal index out of range";
+          return FS_ERR_INVALID;
+        }
+        if (nt && ti[k] >= nt) {
+          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": texcoord index out of range";
+          return FS_ERR_INVALID;
+        }
+      }
+      DevTri& t = mtris[f];
+      std::memset(&t, 0, sizeof(t));
+      t.face = f;
+      if (need) {
+        f3 p0 = verts[vi[0]], p1 = verts[vi[1]], p2 = verts[vi[2]];
+        put3(t.p1, p0);
+        put3(t.p2, p1);
+        put3(t.p3, p2);
+        put4(t.plane, plane_np(calc_normal(p0, p1, p2), p0));  // mesh.cpp:136-146
+      }
+      if (nn)
+        for (int k = 0; k < 3; k++) put3(&mnormals[12 * (size_t)f + 4 * k], normals[ni[k]]);
+    }
+    mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
+    if (!mesh_out[mi].tree) continue;
+    if (S.tris.size() + m.num_triangles > kMaxTriangles) {
+      *err = "too many triangles for the 24-bit leaf encoding";
+      return FS_ERR_INVALID;
+    }
+    std::vector<Prim> prims(m.num_triangles);
+    for (uint32_t f = 0; f < m.num_triangles; f++) {
+      Prim& p = prims[f];
+      p.box.grow(mtris[f].p1);
+      p.box.grow(mtris[f].p2);
+      p.box.grow(mtris[f].p3);
+      for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
+      p.face = f;
+    }
+    for (DevTri& t : mtris) t.mesh_obj = mi;
+    BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &mtris, &mnormals);
+    mesh_out[mi].root = builder.build(prims, &S.max_depth);
+  }
+
+  S.objects.resize(d->num_objects);
+  for (uint32_t i = 0; i < d->num_objects; i++) {
+    const fs_object& o = d->objects[i];
+    if (o.material < 0 || (uint32_t)o.material >= d->num_materials) {
+      *err = "object " + std::to_string(i) + " has no valid material";
+      return FS_ERR_INVALID;
+    }
+    if (o.kind == FS_OBJ_MESH) {
+      if (o.mesh < 0 || (uint32_t)o.mesh >= d->num_meshes) {
+        *err = "object " + std::to_string(i) + " references a missing mesh";
+        return FS_ERR_INVALID;
+      }
+      DevObject& D = S.objects[i];
+      std::memset(&D, 0, sizeof(D));
+      const MeshOut& mo = mesh_out[o.mesh];
+      D.kind = FS_OBJ_MESH;
+      D.mat = o.material;
+      D.i0 = (int32_t)mo.root;
+      D.i1 = mo.normals ? 1 : 0;
+      D.i2 = mo.tree ? 1 : 0;
+      put3(D.d, mo.rb.mn);
+      put3(D.d + 3, mo.rb.mx);
+    } else {
+      int rc = build_object(o, &S.objects[i], err);
+      if (rc) return rc;
+    }
+  }
+  S.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return FS_OK;
+}
+
+}  // namespace fs

@@ -1,0 +1,81 @@
+// fs_scene.h — device-side scene layout (SoA records in HBM) and the host
+// preparation step that builds it from an fs_scene_desc.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "fs_math.h"
+#include "fs_trace.h"
+
+namespace fs {
+
+// Object record, 128 B; read wave-uniformly by the object loop of
+// Scene::Trace (scene.cpp:231-233), so it is fetched with scalar loads.
+struct DevObject {
+  int32_t kind;  // fs_object_kind (QUAD_PUV is stored as QUAD_ONWH)
+  int32_t mat;
+  int32_t i0;    // MESH: BVH root node index
+  int32_t i1;    // MESH: 1 if the mesh has vertex normals
+  int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
+  int32_t i3, i4, i5;
+  float d[24];
+  // SPHERE  d0-2 center, d3 radius
+  // PLANE   d0-3 plane
+  // DISC    d0-3 plane, d4-6 origin, d7 radius
+  // CUBOID  d0-23 six face planes (volume.cpp:234-247)
+  // QUAD    d0-3 plane, d4-6 origin, d7 half width, d8 half height,
+  //         d9-11 bitangent, d12-14 tangent
+  // MESH    d0-5 reference root bounds (min, max) — mesh.cpp:129-133
+};
+static_assert(sizeof(DevObject) == 128, "DevObject layout");
+
+// BVH2 node, 64 B: both child boxes (SoA over the two children) + child words.
+// Child word: bit31 set -> leaf, bits 24..30 = triangle count, bits 0..23 =
+// first triangle; otherwise an inner-node index.
+struct BvhNode {
+  float lo_x[2], hi_x[2];
+  float lo_y[2], hi_y[2];
+  float lo_z[2], hi_z[2];
+  uint32_t child[2];
+  uint32_t pad[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kMaxLeafCount = 127;
+constexpr uint32_t kMaxTriangles = 1u << 24;
+constexpr uint32_t kTraversalStack = 32;  // BVH depth bound (builder enforces)
+
+// Triangle record, 64 B: the reference test operands (intersect.cpp:357-419)
+// — the three corners in the reference's reversed winding plus the
+// precomputed face plane (mesh.cpp:136-146) — and the face index (tie-break).
+struct DevTri {
+  float p1[3];
+  uint32_t face;
+  float p2[3];
+  uint32_t mesh_obj;
+  float p3[3];
+  float pad;
+  float plane[4];
+};
+static_assert(sizeof(DevTri) == 64, "DevTri layout");
+
+struct PreparedScene {
+  std::vector<DevObject> objects;
+  std::vector<BvhNode> nodes;
+  std::vector<DevTri> tris;
+  std::vector<float> tri_normals;  // 12 floats per triangle (n0,n1,n2 + pad) or empty
+  std::vector<fs_material> materials;
+  std::vector<float> table;        // 4 floats per entry
+  int32_t sky = 0;
+  uint32_t max_depth = 0;
+  double build_ms = 0.0;
+};
+
+// Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
+// one SAH BVH per mesh. Returns FS_OK or an fs_status with *err set.
+int prepare_scene(const fs_scene_desc* desc, PreparedScene* out, std::string* err);
+
+}  // namespace fs

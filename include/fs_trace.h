@@ -1,0 +1,257 @@
+/*
+ * fs_trace.h — C ABI of the MI355X path-trace layer (libfsgpu.so).
+ *
+ * Drop-in boundary for the reference's per-pixel Monte-Carlo path tracer
+ * (ramenhut/final-stage-path-tracer-2-0). The reference entry point this layer
+ * replaces is
+ *
+ *     void base::TraceScene(const Camera&, Scene*, DisplayFrame*,
+ *                           ImagePlaneCache* = nullptr);      engine.h:74-75
+ *
+ * which adds ONE jittered sample per pixel to a running-mean frame
+ * (engine.cpp:253-296, frame.cpp:53-85). The repo's C++ mirror of that API
+ * (final-stage-path-tracer-2-0_amd/host/engine.h) calls the functions below.
+ *
+ * Conventions: plain C types only; every function returns 0 on success and a
+ * negative fs_status on failure (fs_last_error() has the message); no C++
+ * exception crosses this boundary; the caller owns every pointer it passes.
+ */
+#ifndef FS_TRACE_H_
+#define FS_TRACE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS_ABI_VERSION 1
+#define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
+#define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
+#define FS_NO_INDEX 0xFFFFFFFFu
+
+typedef enum fs_status {
+  FS_OK = 0,
+  FS_ERR_INVALID = -1,  /* bad argument / malformed scene */
+  FS_ERR_DEVICE = -2,   /* HIP runtime error */
+  FS_ERR_NOMEM = -3,    /* allocation failed */
+  FS_ERR_STATE = -4,    /* call out of order (e.g. render before upload) */
+  FS_ERR_COMM = -5,     /* RCCL error */
+  FS_ERR_IO = -6        /* file could not be read */
+} fs_status;
+
+/* Material kinds: the nine classes of material.h:54-328. */
+typedef enum fs_material_kind {
+  FS_MAT_DIFFUSE = 0, /* DiffuseMaterial  material.cpp:55-137  */
+  FS_MAT_LIGHT = 1,   /* LightMaterial    material.cpp:28-53   */
+  FS_MAT_METAL = 2,   /* MetalMaterial    material.cpp:139-170 */
+  FS_MAT_MIRROR = 3,  /* MirrorMaterial   material.cpp:172-190 */
+  FS_MAT_GLASS = 4,   /* GlassMaterial    material.cpp:192-221 */
+  FS_MAT_LIQUID = 5,  /* LiquidMaterial   material.cpp:223-250 */
+  FS_MAT_CERAMIC = 6, /* CeramicMaterial  material.cpp:252-282 */
+  FS_MAT_GLOW = 7,    /* GlowMaterial     material.cpp:284-301 */
+  FS_MAT_FOG = 8      /* FogMaterial      material.cpp:303-339 */
+} fs_material_kind;
+
+/* One material instance, field names follow the reference members. */
+typedef struct fs_material {
+  int32_t kind;         /* fs_material_kind */
+  uint32_t id;          /* Material::material_id_ = random_integer() (material.cpp:26) */
+  float diffuse[3];     /* diffuse_ */
+  float emissive[3];    /* LightMaterial::emissive_ */
+  float glow[3];        /* GlowMaterial::glow_ */
+  float roughness;      /* MetalMaterial::roughness_ */
+  float shininess;      /* CeramicMaterial::shininess_ */
+  float index;          /* Glass/Liquid index_ */
+  float reflectivity;   /* Glass/Liquid reflectivity_ */
+  float frost;          /* GlassMaterial::frost_ */
+  float density;        /* FogMaterial::density_ (already x1000, material.cpp:306) */
+  int32_t texture;      /* index into fs_scene_desc.textures, or -1 */
+  float texture_scale;  /* texture_scale_ */
+} fs_material;
+
+/* Object kinds: the constructors of object.h / mesh.h, arguments verbatim. */
+typedef enum fs_object_kind {
+  FS_OBJ_SPHERE = 0,   /* SphericalObject(origin, radius)            object.cpp:17 */
+  FS_OBJ_PLANE = 1,    /* PlanarObject(plane)                        object.cpp:38 */
+  FS_OBJ_DISC = 2,     /* DiscObject(origin, normal, radius)         object.cpp:75 */
+  FS_OBJ_CUBOID = 3,   /* CuboidObject(origin, w, h, d) [+Rotate]    object.cpp:115-124 */
+  FS_OBJ_QUAD_ONWH = 4,/* QuadObject(origin, normal, width, height)  object.cpp:167 */
+  FS_OBJ_QUAD_PUV = 5, /* QuadObject(position, u, v)                 object.cpp:191 */
+  FS_OBJ_MESH = 6      /* MeshObject(file, invert, T, S, R)          mesh.cpp:168 */
+} fs_object_kind;
+
+/*
+ * Constructor arguments, by kind (a[] layout):
+ *  SPHERE    a[0..2]=origin a[3]=radius
+ *  PLANE     a[0..3]=plane (nx,ny,nz,w)
+ *  DISC      a[0..2]=origin a[3..5]=normal a[6]=radius
+ *  CUBOID    a[0..2]=origin a[3]=width a[4]=height a[5]=depth;
+ *            if rotate!=0: CuboidObject::Rotate(axis=a[6..8], angle=a[9])
+ *            (ParseCuboid always calls Rotate, scene.cpp:452)
+ *  QUAD_ONWH a[0..2]=origin a[3..5]=normal a[6]=width a[7]=height
+ *  QUAD_PUV  a[0..2]=position a[3..5]=u a[6..8]=v
+ *  MESH      mesh = index into fs_scene_desc.meshes
+ */
+typedef struct fs_object {
+  int32_t kind;     /* fs_object_kind */
+  int32_t material; /* index into fs_scene_desc.materials; must be >= 0 */
+  int32_t mesh;     /* FS_OBJ_MESH only */
+  int32_t rotate;   /* FS_OBJ_CUBOID only */
+  float a[12];
+} fs_object;
+
+/*
+ * A mesh as tinyobj hands it to MeshObject::MeshObject (mesh.cpp:168-275):
+ * raw OBJ attribute arrays plus triangle corner indices in OBJ order. The
+ * constructor math (T*R*S bake, normal normalisation/inversion, winding
+ * reversal, face planes) is applied by the consumer, exactly as the reference.
+ */
+typedef struct fs_mesh {
+  const float* positions;   /* 3 floats per vertex */
+  uint32_t num_positions;
+  const float* normals;     /* 3 floats per normal, may be NULL */
+  uint32_t num_normals;
+  const float* texcoords;   /* 2 floats per texcoord, may be NULL */
+  uint32_t num_texcoords;
+  /* 9 int32 per triangle: (v0,n0,t0, v1,n1,t1, v2,n2,t2), -1 = absent */
+  const int32_t* corners;
+  uint32_t num_triangles;
+  int32_t invert_normals;
+  float translation[3];
+  float scale[3];
+  float rotation[4];        /* <x,y,z> axis, w angle (radians) */
+} fs_mesh;
+
+typedef struct fs_texture {
+  const float* rgb; /* width*height*3 floats, row-major */
+  uint32_t width;
+  uint32_t height;
+} fs_texture;
+
+typedef struct fs_scene_desc {
+  const fs_material* materials; /* Material instances in creation order */
+  uint32_t num_materials;
+  int32_t sky_material;         /* index of the sky (Scene::sky_material_) */
+  const fs_object* objects;     /* Scene::object_list_ order (scene.cpp:231) */
+  uint32_t num_objects;
+  const fs_mesh* meshes;
+  uint32_t num_meshes;
+  const fs_texture* textures;
+  uint32_t num_textures;
+  /* normal_sphere table (normal.cpp:9-27), FS_NORMAL_TABLE_SIZE x 3 floats */
+  const float* normal_table;
+} fs_scene_desc;
+
+/* Camera POD, camera.h:43-63. */
+typedef struct fs_camera {
+  float origin[3];
+  float target[3];
+  float fov_y;         /* degrees */
+  float aperture_size; /* > 0 enables the thin lens (engine.cpp:221) */
+  float focal_depth;
+  float z_near;
+  float z_far;
+  int32_t fast_render; /* engine.cpp:68-70 */
+} fs_camera;
+
+/*
+ * One render call = `spp` consecutive calls of the reference TraceScene on the
+ * pixels this rank owns. Sample k (k = sample_base .. sample_base+spp-1) of
+ * pixel (x, y) draws from the xorshift64* stream seeded with
+ *     splitmix64(((uint64)(y*width + x) << 20) ^ k ^ seed) | 1
+ * (per-(pixel,sample) seeding replaces the reference's clock seed,
+ * engine.cpp:179, so renders are reproducible and shardable). Row y = 0 is the
+ * bottom of the image, as in the reference frame (engine.cpp:215).
+ *
+ * Ownership: the frame is cut into tile_size x tile_size tiles numbered
+ * row-major; this call renders tiles t with t % tile_stride == tile_offset.
+ */
+typedef struct fs_render_params {
+  uint32_t width;
+  uint32_t height;
+  uint32_t spp;
+  uint32_t sample_base;
+  uint64_t seed;
+  uint32_t tile_size;   /* 0 -> 64 */
+  uint32_t tile_offset; /* rank */
+  uint32_t tile_stride; /* world size (0 -> 1) */
+  uint32_t flags;       /* FS_RENDER_* */
+} fs_render_params;
+
+#define FS_RENDER_COUNTERS 1u /* accumulate traversal counters (slower) */
+
+/* Device-resident DisplayFrame (frame.h:49-92), row y=0 at the bottom. */
+typedef enum fs_frame_plane {
+  FS_PLANE_COLOR = 0,    /* float32 x3  render_target_ (running mean) */
+  FS_PLANE_COUNT = 1,    /* uint32      count_buffer_ */
+  FS_PLANE_DISPLAY = 2,  /* uint8 x3    display_buffer_ (gamma 2.2) */
+  FS_PLANE_NORMAL = 3,   /* float32 x3  normal_buffer_ */
+  FS_PLANE_DEPTH = 4,    /* float32     depth_buffer_ */
+  FS_PLANE_MATERIAL = 5  /* uint64      material_id_buffer_ */
+} fs_frame_plane;
+
+/* Traversal / work counters (FS_RENDER_COUNTERS). */
+typedef struct fs_counters {
+  uint64_t samples;
+  uint64_t segments;    /* ray segments traced (closest-hit queries) */
+  uint64_t node_visits; /* BVH nodes whose boxes were tested */
+  uint64_t tri_tests;   /* ray/triangle tests */
+  uint64_t prim_tests;  /* analytic object tests */
+} fs_counters;
+
+typedef struct fs_context fs_context;
+typedef struct fs_frame fs_frame;
+
+/* ---- context ---------------------------------------------------------- */
+int fs_abi_version(void);
+const char* fs_last_error(void);                  /* thread-local message */
+int fs_device_count(int* count);
+int fs_create(int device, fs_context** out);
+int fs_destroy(fs_context* ctx);
+
+/* Copies the scene, builds per-mesh BVHs on the host and uploads SoA arrays.
+ * Replaces any scene previously uploaded to ctx. */
+int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc);
+/* Host BVH build + upload time of the last fs_upload_scene, in ms. */
+int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms,
+                   uint64_t* num_triangles, uint64_t* num_nodes,
+                   uint64_t* device_bytes);
+
+/* ---- frames ----------------------------------------------------------- */
+int fs_frame_create(fs_context* ctx, uint32_t width, uint32_t height,
+                    fs_frame** out);
+int fs_frame_destroy(fs_frame* frame);
+int fs_frame_reset(fs_frame* frame);              /* DisplayFrame::Reset */
+/* Copies one plane (all pixels) to host memory of the plane's byte size. */
+int fs_frame_read(fs_frame* frame, int plane, void* host_dst, size_t bytes);
+/* Overwrites one plane from host memory (resume / test setup). */
+int fs_frame_write(fs_frame* frame, int plane, const void* host_src,
+                   size_t bytes);
+
+/* ---- the hot path ------------------------------------------------------ */
+/* Adds params->spp samples per owned pixel into frame; asynchronous on the
+ * context stream; fs_synchronize() waits. counters may be NULL. */
+int fs_render(fs_context* ctx, const fs_camera* camera,
+              const fs_render_params* params, fs_frame* frame);
+int fs_synchronize(fs_context* ctx);
+int fs_read_counters(fs_context* ctx, fs_counters* out); /* and zero them */
+/* Device time of the last fs_render's trace kernel(s) in ms (HIP events). */
+int fs_last_render_ms(fs_context* ctx, float* ms);
+
+/* ---- multi-GPU (RCCL over xGMI) ---------------------------------------- */
+#define FS_COMM_ID_BYTES 128
+int fs_comm_unique_id(uint8_t id[FS_COMM_ID_BYTES]);
+int fs_comm_init(fs_context* ctx, int nranks, int rank,
+                 const uint8_t id[FS_COMM_ID_BYTES]);
+/* Gathers every rank's owned tiles (per params' tiling) into root's frame. */
+int fs_frame_gather(fs_context* ctx, fs_frame* frame,
+                    const fs_render_params* params, int root);
+int fs_comm_destroy(fs_context* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FS_TRACE_H_ */
