@@ -1,0 +1,227 @@
+"""Benchmark: Msamples/s of the path-trace hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+A step is one full render of the workload frame (W x H pixels x spp samples,
+the reference's TraceScene called spp times, engine.cpp:253) into a reset
+frame; for N > 1 the frame's 64x64 tiles are dealt round-robin to the ranks
+and gathered to rank 0 with RCCL (ncclGather over xGMI) inside the step.
+Rank 0 prints one JSON line. Scene load/BVH build are outside the timed
+region (reported in config).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "final-stage-path-tracer-2-0_amd")
+sys.path.insert(0, PKG)
+
+# Load the HIP layer before anything else can pull in another HIP runtime.
+import fsamd  # noqa: E402
+import scenes  # noqa: E402
+
+METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080, 1024spp; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+WORKLOADS = {
+    "c4": "~1M-triangle displaced blob + Ceramic/Glass spheres + Metal cuboid in the Cornell room "
+          "(BASELINE configs[3] scene; SURVEY §8d C4) at 1920x1080, 1024 spp",
+    "c2": "Cornell box + glossy (Ceramic) + glass spheres (BASELINE configs[1]) at 1920x1080, 1024 spp",
+    "c3": "~250k-triangle procedural atrium (BASELINE configs[2]) at 1920x1080, 1024 spp",
+}
+# Algorithmic bytes per unit of work, from the device SoA record
+# sizes: BVH node 64 B, triangle 64 B, analytic object record 128 B, per
+# segment one material record (76 B) + one normal-table entry (16 B); per
+# sample 12 B of radiance.
+S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--cpu-spp", type=int, default=1, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-tile-stride", type=int, default=4, help="CPU sample renders 1/stride of the tiles")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--scene-dir", default=None)
+    return ap.parse_args()
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch  # noqa: F401  (CPU-only use: gloo control plane)
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    scene_dir = args.scene_dir or os.path.join(tempfile.gettempdir(), f"fs_bench_{os.getuid()}_r{rank}")
+    t0 = time.time()
+    path = scenes.write(args.scene, os.path.join(scene_dir, args.scene))
+    fsamd.reset_main_rng()
+    scene = fsamd.HostScene.load(path)
+    fsamd.initialize_materials()
+    cam = scene.camera(0)
+    gen_s = time.time() - t0
+    r = fsamd.Renderer(local_rank)
+    r.upload(scene)
+    stats = r.scene_stats()
+    log(f"rank {rank}: scene {args.scene} written+loaded in {gen_s:.1f}s, BVH {stats}")
+    W, H, spp = args.width, args.height, args.spp
+    frame = r.frame(W, H)
+    params = fsamd.render_params(W, H, spp, tile_offset=rank, tile_stride=world)
+    if world > 1:
+        import torch
+
+        uid = bytearray(fsamd.Renderer.comm_unique_id() if rank == 0 else bytes(128))
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        r.comm_init(world, rank, bytes(t.tolist()))
+
+    def step():
+        frame.reset()
+        r.render(cam, frame, spp=spp, tile_offset=rank, tile_stride=world, sync=False)
+        if world > 1:
+            r.gather(frame, params, root=0)
+        r.synchronize()
+        return r.last_render_ms()
+
+    for i in range(args.warmup):
+        ms = step()
+        log(f"rank {rank}: warmup {i} render {ms:.1f} ms")
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    barrier()
+    r.synchronize()
+    kernel_ms = []
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        kernel_ms.append(step())
+        log(f"rank {rank}: step {i} render {kernel_ms[-1]:.1f} ms")
+    r.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        import torch
+
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # ---- roofline of the trace kernel: algorithmic bytes from a counted launch
+    total_samples = W * H * spp * args.steps
+    value = total_samples / elapsed / 1e6
+    cf = r.frame(W, H)
+    cspp = 8
+    r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
+    c = r.counters()
+    cf.close()
+    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * c["tri_tests"] + S_PRIM * c["prim_tests"]
+                        + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
+    chunk = 32  # fs_render splits a step into launches of 32 spp (fs_device.hip)
+    launches = (spp + chunk - 1) // chunk
+    avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
+    owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
+    per_launch_bytes = bytes_per_sample * owned_samples / launches
+    achieved = per_launch_bytes / avg_launch_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}.json")
+    if os.path.exists(pmc) and spp == 1024:
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "render_kernel<false>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "bytes_per_sample": round(bytes_per_sample, 1),
+                "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
+                "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),
+                "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, scene, cam)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded procedural scene, per-(pixel,sample) seeded xorshift64*)",
+            "config": {"workload": WORKLOADS[args.scene], "scene": args.scene, "width": W, "height": H,
+                       "spp": spp, "triangles": stats["triangles"], "bvh_nodes": stats["nodes"],
+                       "bvh_build_ms": round(stats["build_ms"], 1),
+                       "parallelism": f"64x64 tiles round-robin over {world} GPU(s)"
+                                      + (" + RCCL ncclGather to rank 0" if world > 1 else "")},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, scene, cam):
+    """The oracle (CPU port of the reference algorithm, reference octree)
+    timed on a bounded tile subset of the same workload."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        t = time.time()
+        o = oracle_py.Scene(scene.desc_ptr())
+        build = time.time() - t
+        stride = args.cpu_tile_stride
+        p = fsamd.render_params(args.width, args.height, args.cpu_spp, tile_stride=stride, tile_offset=0)
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        t = time.perf_counter()
+        f = o.render(cam, p, threads=threads)
+        dt = time.perf_counter() - t
+        n = f.stats["samples"]
+        o.close()
+        cpu_model = ""
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+        return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+                "sample": f"{args.scene} {args.width}x{args.height}, 1/{stride} of the 64x64 tiles, "
+                          f"{args.cpu_spp} spp = {n} samples in {dt:.1f}s (octree build {build:.1f}s excluded)",
+                "cpu": cpu_model or platform.processor()}
+    except Exception as e:  # the baseline is reported, never required
+        log(f"cpu baseline failed: {e}")
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round profiling script (runs on the GPU box from the repo root).
+set -o pipefail
+R=${1:-r01}
+mkdir -p gpurun_out/$R
+export TMPDIR=/tmp
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$R/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/$R/smoke.log; exit 1; }
+timeout -k 10 600 python bench.py > gpurun_out/$R/bench.json 2> gpurun_out/$R/bench.err || { echo bench failed; tail -20 gpurun_out/$R/bench.err; exit 1; }
+cat gpurun_out/$R/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$R/prof -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu > gpurun_out/$R/prof_bench.json 2> gpurun_out/$R/prof.err || { echo rocprof failed; tail -20 gpurun_out/$R/prof.err; exit 1; }
+find gpurun_out/$R/prof -name "*stats*" | head
