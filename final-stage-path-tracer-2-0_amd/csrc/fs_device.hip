@@ -8,6 +8,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -91,9 +92,16 @@ __device__ __forceinline__ bool ref_slab(float s, float v, float mn, float mx, f
 __device__ __forceinline__ bool ref_bounds_worker(f3 mn, f3 mx, f3 s, f3 e, float& param) {
   f3 v = e - s;
   float fnear = -kInfinity, ffar = kInfinity;
-  if (!ref_slab(s.x, v.x, mn.x, mx.x, fnear, ffar)) return false;
-  if (!ref_slab(s.y, v.y, mn.y, mx.y, fnear, ffar)) return false;
-  if (!ref_slab(s.z, v.z, mn.z, mx.z, fnear, ffar)) return false;
+  // One slab per iteration, not unrolled: the three IEEE divisions stay
+  // sequential and do not inflate the register footprint of the caller.
+#pragma unroll 1
+  for (int a = 0; a < 3; a++) {
+    float sa = a == 0 ? s.x : (a == 1 ? s.y : s.z);
+    float va = a == 0 ? v.x : (a == 1 ? v.y : v.z);
+    float lo = a == 0 ? mn.x : (a == 1 ? mn.y : mn.z);
+    float hi = a == 0 ? mx.x : (a == 1 ? mx.y : mx.z);
+    if (!ref_slab(sa, va, lo, hi, fnear, ffar)) return false;
+  }
   if (fnear > ffar) return false;
   if (ffar < 0 || fnear < 0 || fnear > 1) return false;
   param = fnear;
@@ -116,14 +124,56 @@ __device__ __forceinline__ bool ref_ray_bounds(f3 mn, f3 mx, const Ray& r, bool 
     param = 0.0f;
     return true;
   }
-  if (si) {
-    if (ref_bounds_worker(mn, mx, r.stop, r.start, param)) {
-      param = 1.0f - param;
-      return true;
+  // Reversed segment when the start is inside (:635-649); selected per
+  // component so both cases share one worker instance.
+  f3 a = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
+  f3 b = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
+  if (!ref_bounds_worker(mn, mx, a, b, param)) return false;
+  if (si) param = 1.0f - param;
+  return true;
+}
+
+// The mesh-root cull of MeshBvhNode::Trace (mesh.cpp:79-83): true when the
+// reference would NOT skip the mesh (ray_intersect_bounds hits and its param
+// is <= best). Slab times use v_rcp (relative error < 3e-7 against the
+// reference's IEEE quotient) after the reference's exact subtraction, so all
+// sign tests are exact; a magnitude comparison within 1e-5 of its threshold
+// is redone with the reference's divisions. Exact by construction.
+__device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best) {
+  bool si = in_bounds(mn, mx, r.start);
+  if (zl) return si;                                 // param 0 (intersect.cpp:604-616)
+  if (si && in_bounds(mn, mx, r.stop)) return true;  // param 0 (:621-630)
+  f3 s = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
+  f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
+  f3 v = e - s;
+  float fnear = -kInfinity, ffar = kInfinity;
+  bool outside = false;
+  auto slab = [&](float sa, float va, float lo, float hi) {
+    if (cmp_eps(va, 0.0f, kEpsilon)) {
+      outside |= (sa < lo || sa > hi);
+      return;
     }
-    return false;
-  }
-  return ref_bounds_worker(mn, mx, r.start, r.stop, param);
+    float rc = __builtin_amdgcn_rcpf(va);
+    float t1 = (lo - sa) * rc, t2 = (hi - sa) * rc;
+    fnear = fmaxf(fnear, fminf(t1, t2));
+    ffar = fminf(ffar, fmaxf(t1, t2));
+  };
+  slab(s.x, v.x, mn.x, mx.x);
+  slab(s.y, v.y, mn.y, mx.y);
+  slab(s.z, v.z, mn.z, mx.z);
+  if (outside || ffar < 0 || fnear < 0) return false;  // exact tests
+  bool unsure = fabsf(fnear - ffar) <= 1e-5f * (fabsf(fnear) + fabsf(ffar));
+  if (!unsure && fnear > ffar) return false;
+  if (fabsf(fnear - 1.0f) <= 1e-5f)
+    unsure = true;
+  else if (fnear > 1) return false;
+  float np = si ? 1.0f - fnear : fnear;
+  if (fabsf(np - best) <= 1e-5f)
+    unsure = true;
+  else if (np > best) return false;
+  if (!unsure) return true;
+  float pe;
+  return ref_ray_bounds(mn, mx, r, zl, pe) && !(pe > best);
 }
 
 // intersect.cpp:96-129 + 146-177: planar map, then barycentrics.
@@ -150,20 +200,36 @@ __device__ __forceinline__ void planar_bary(f4 pl, f3 v0, f3 v1, f3 vp, float& u
 }
 
 struct TriData {
-  f3 p1, p2, p3;
+  f3 p1, v0, v1;
+  float d00, d01, d11, inv;
+  uint32_t axis, face;
   f4 pl;
-  uint32_t face;
 };
 __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
   const float4* q = reinterpret_cast<const float4*>(T + i);
-  float4 a = q[0], b = q[1], c = q[2], d = q[3];
+  float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   TriData t;
   t.p1 = mk3(a.x, a.y, a.z);
-  t.p2 = mk3(b.x, b.y, b.z);
-  t.p3 = mk3(c.x, c.y, c.z);
-  t.pl = mk4(d.x, d.y, d.z, d.w);
   t.face = __float_as_uint(a.w);
+  t.v0 = mk3(b.x, b.y, b.z);
+  t.d00 = b.w;
+  t.v1 = mk3(c.x, c.y, c.z);
+  t.d01 = c.w;
+  t.d11 = d.x;
+  t.inv = d.y;
+  t.axis = __float_as_uint(d.z);
+  t.pl = mk4(e.x, e.y, e.z, e.w);
   return t;
+}
+// intersect.cpp:146-177 with the triangle-only terms precomputed: vp is
+// planar-mapped like v0/v1 and the reference's dot products follow.
+__device__ __forceinline__ void bary_pre(const TriData& T, f3 vp, float& u, float& v) {
+  if (T.axis == 0) vp.x = 0;
+  if (T.axis == 1) vp.y = 0;
+  if (T.axis == 2) vp.z = 0;
+  float d02 = dot(T.v0, vp), d12 = dot(T.v1, vp);
+  u = (T.d11 * d02 - T.d01 * d12) * T.inv;
+  v = (T.d00 * d12 - T.d01 * d02) * T.inv;
 }
 
 // intersect.cpp:357-419 (non-zero-length branch)
@@ -172,7 +238,7 @@ __device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t
   f3 pp;
   if (!ray_plane(T.pl, r, tt, pp)) return false;
   float uu, vv;
-  planar_bary(T.pl, T.p2 - T.p1, T.p3 - T.p1, pp - T.p1, uu, vv);
+  bary_pre(T, pp - T.p1, uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     t = tt;
     p = pp;
@@ -188,7 +254,7 @@ __device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, 
   float d4 = T.pl.x * pt.x + T.pl.y * pt.y + T.pl.z * pt.z + T.pl.w * 1.0f;
   if (!cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) return false;
   float uu, vv;
-  planar_bary(T.pl, T.p2 - T.p1, T.p3 - T.p1, pt - T.p1, uu, vv);
+  bary_pre(T, pt - T.p1, uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     u = uu;
     v = vv;
@@ -321,10 +387,9 @@ __device__ bool scene_trace(const DevScene& S, const Ray& r, Hit& h, uint32_t* _
     const float* d = o->d;
     if (kind == FS_OBJ_MESH) {
       if (!o->i2) continue;
-      float np;
       // MeshBvhNode::Trace root test (mesh.cpp:79-83), restated exactly: the
       // reference skips the mesh when the root box "param" exceeds the best.
-      if (!ref_ray_bounds(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, np) || np > h.t) continue;
+      if (!ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) continue;
       float before = h.t;
       int32_t before_obj = h.obj;
       traverse_mesh<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, mat, r, zl, h, stk, tally);
@@ -423,6 +488,15 @@ __device__ __forceinline__ f3 random_refraction(const DevScene& S, f3 inc, f3 n,
   return rotate(refl, cosf(delta), sinf(delta), axis);
 }
 
+// Ceramic's specular term (float)pow((double)(h.n), 50) (material.cpp:280).
+// Computed by repeated squaring in double: within ~1e-15 relative of the
+// correctly rounded pow, so the float result is the same except when the
+// double lies that close to a float rounding tie (never seen in the tests).
+__device__ __forceinline__ float pow50(float xf) {
+  double x = xf, x2 = x * x, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8, x32 = x16 * x16;
+  return (float)(x32 * x16 * x2);
+}
+
 // Material::Reflection (material.cpp)
 __device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, f3 view, f3 n, uint64_t& rng) {
   switch (m.kind) {
@@ -471,13 +545,8 @@ __device__ __forceinline__ uint32_t mat_of(uint32_t lo, uint32_t hi, int k) {
   return (k < 4 ? (lo >> (8 * k)) : (hi >> (8 * (k - 4)))) & 0xFFu;
 }
 
-// One sample = TracePixel (engine.cpp:161-164) after the ray generation of
-// engine.cpp:210-244. Returns the TraceResult colour.
-template <bool COUNT>
-__device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, float fy, uint64_t rng, Aov& aov,
-                           uint32_t* __restrict__ stk, float2* __restrict__ lvl, Tally<COUNT>& tally,
-                           uint32_t& segments) {
-  // ---- camera ray (engine.cpp:210-244)
+// engine.cpp:210-244: jittered ray through the pixel, optional thin lens.
+__device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy, uint64_t& rng) {
   float jx = (float)((double)rng_float(rng) - 0.5);
   float jy = (float)((double)rng_float(rng) - 0.5);
   float xd = (float)((double)C.hpw * ((double)((fx + jx) / (C.width - 1)) * 2.0 - 1.0));
@@ -500,73 +569,19 @@ __device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, floa
     }
   }
 
-  // ---- forward pass: TraceStep recursion descending (engine.cpp:59-138)
-  uint32_t mats_lo = 0, mats_hi = 0;
-  f3 L = mk3(0, 0, 0);
-  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-  int top = -1;
-  for (uint32_t depth = 0;; depth++) {
-    if (depth >= kMaxDepth) {
-      L = mk3(0, 0, 0);
-      break;
-    }
-    if (C.fast_render && depth > 1) {
-      L = mk3(1, 1, 1);
-      break;
-    }
-    segments++;
-    Hit h;
-    if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
-      if (depth == 1) lp0 = r.stop;
-      L = mk3(S.sky_r, S.sky_g, S.sky_b);
-      if (depth == 0) {
-        aov.normal = normalize(r.dir);
-        aov.id = S.sky_id;
-        aov.depth = C.z_far;
-      }
-      break;
-    }
-    if (depth == 1) lp0 = h.p;
-    const fs_material& m = S.materials[h.mat];
-    int32_t kind = m.kind;
-    f3 view = normalize(h.p - r.start);
-    f3 refl = mat_reflection(S, m, view, h.n, rng);
-    float c = fmaxf(0.0f, dot(h.n, refl));
-    float ds = 0.0f;
-    if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
-      f3 hv = normalize(view * (float)-1.0 + refl);
-      ds = (float)pow((double)dot(hv, h.n), 50.0);
-    }
-    lvl[depth * kBlock] = make_float2(c, ds);
-    if (depth < 4)
-      mats_lo |= (uint32_t)h.mat << (8 * depth);
-    else
-      mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
-    top = (int)depth;
-    if (depth == 0) {
-      p0 = h.p;
-      aov.normal = h.n;
-      aov.id = m.id;
-      aov.depth = length(r.start - h.p);
-    }
-    Ray nr;  // engine.cpp:120-127
-    nr.start = h.p;
-    nr.stop = h.p + refl * C.z_far;
-    nr.dir = nr.stop - nr.start;
-    f3 off = refl * kStepOffset;
-    nr.start = nr.start + off;
-    nr.dir = nr.dir - off;
-    if (!mat_will_use(m, refl, h.n)) {
-      L = mk3(0, 0, 0);
-      break;
-    }
-    r = nr;
-  }
+  return r;
+}
 
-  // ---- backward pass: Material::Sample in the recursion's return order
+// One sample = TracePixel (engine.cpp:161-164) after the ray generation of
+// engine.cpp:210-244. Returns the TraceResult colour.
+// Backward pass: Material::Sample in the order the TraceStep recursion
+// returns (engine.cpp:141-156); L enters as the radiance of level `top`+1.
+__device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t mats_lo, uint32_t mats_hi,
+                                     const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
+                                     int stride = kBlock) {
   for (int k = top; k >= 0; --k) {
     const fs_material& m = S.materials[mat_of(mats_lo, mats_hi, k)];
-    float2 cs = lvl[k * kBlock];
+    float2 cs = lvl[k * stride];
     f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
     switch (m.kind) {
       case FS_MAT_LIGHT:
@@ -609,6 +624,78 @@ __device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, floa
     if (length(L) > 10.0f && m0.kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
   }
   return L;
+}
+
+template <bool COUNT>
+__device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, float fy, uint64_t rng, Aov& aov,
+                           uint32_t* __restrict__ stk, float2* __restrict__ lvl, Tally<COUNT>& tally,
+                           uint32_t& segments) {
+  Ray r = camera_ray(C, fx, fy, rng);
+
+  // ---- forward pass: TraceStep recursion descending (engine.cpp:59-138)
+  uint32_t mats_lo = 0, mats_hi = 0;
+  f3 L = mk3(0, 0, 0);
+  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
+  int top = -1;
+  for (uint32_t depth = 0;; depth++) {
+    if (depth >= kMaxDepth) {
+      L = mk3(0, 0, 0);
+      break;
+    }
+    if (C.fast_render && depth > 1) {
+      L = mk3(1, 1, 1);
+      break;
+    }
+    segments++;
+    Hit h;
+    if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
+      if (depth == 1) lp0 = r.stop;
+      L = mk3(S.sky_r, S.sky_g, S.sky_b);
+      if (depth == 0) {
+        aov.normal = normalize(r.dir);
+        aov.id = S.sky_id;
+        aov.depth = C.z_far;
+      }
+      break;
+    }
+    if (depth == 1) lp0 = h.p;
+    const fs_material& m = S.materials[h.mat];
+    int32_t kind = m.kind;
+    f3 view = normalize(h.p - r.start);
+    f3 refl = mat_reflection(S, m, view, h.n, rng);
+    float c = fmaxf(0.0f, dot(h.n, refl));
+    float ds = 0.0f;
+    if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
+      f3 hv = normalize(view * (float)-1.0 + refl);
+      ds = pow50(dot(hv, h.n));
+    }
+    lvl[depth * kBlock] = make_float2(c, ds);
+    if (depth < 4)
+      mats_lo |= (uint32_t)h.mat << (8 * depth);
+    else
+      mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
+    top = (int)depth;
+    if (depth == 0) {
+      p0 = h.p;
+      aov.normal = h.n;
+      aov.id = m.id;
+      aov.depth = length(r.start - h.p);
+    }
+    Ray nr;  // engine.cpp:120-127
+    nr.start = h.p;
+    nr.stop = h.p + refl * C.z_far;
+    nr.dir = nr.stop - nr.start;
+    f3 off = refl * kStepOffset;
+    nr.start = nr.start + off;
+    nr.dir = nr.dir - off;
+    if (!mat_will_use(m, refl, h.n)) {
+      L = mk3(0, 0, 0);
+      break;
+    }
+    r = nr;
+  }
+
+  return unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng);
 }
 
 __device__ __forceinline__ uint8_t gamma8(float c) {  // frame.cpp:67-71
@@ -675,6 +762,612 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
     atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
     atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
   }
+}
+
+
+// Path regeneration: one loop iteration traces ONE ray segment for every
+// active lane; a lane whose path ended unwinds it, folds it into the running
+// mean and starts its pixel's next sample at once, so a wave never idles
+// waiting for its longest path (the forward/backward split keeps the
+// reference's rounding). Same outputs as render_kernel, bit for bit.
+template <bool COUNT, int WAVES>
+__global__ __launch_bounds__(kBlock, WAVES) void render_kernel_regen(DevScene S, DevCamera C, DevFrame F, Launch P,
+                                                               DevCounters* __restrict__ counters) {
+  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  __shared__ float2 lvl_all[kMaxDepth * kBlock];
+  const uint32_t lane = threadIdx.x;
+  uint32_t* stk = stk_all + lane;
+  float2* lvl = lvl_all + lane;
+
+  const uint32_t micro_per_side = P.tile_size / 8;
+  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t owned = blockIdx.x / micro_per_tile;
+  const uint32_t micro = blockIdx.x % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const uint32_t x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+  const uint32_t y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  if (x >= F.width || y >= F.height) return;
+
+  const size_t pix = (size_t)y * F.width + x;
+  const float fx = (float)x, fy = (float)y;
+  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
+  uint32_t n = F.count[pix];
+  Aov aov;
+  aov.normal = mk3(0, 0, 0);
+  aov.depth = 0.0f;
+  aov.id = 0;
+  Tally<COUNT> tally;
+  uint32_t segments = 0;
+
+  uint32_t s = 0;
+  uint64_t rng = 0;
+  Ray r;
+  uint32_t depth = 0, mats_lo = 0, mats_hi = 0;
+  int top = -1;
+  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
+  bool fresh = true;
+  while (s < P.spp) {
+    if (fresh) {  // TracePixel for sample s (engine.cpp:161-164)
+      rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
+      r = camera_ray(C, fx, fy, rng);
+      depth = 0;
+      mats_lo = mats_hi = 0;
+      top = -1;
+      p0 = lp0 = mk3(0, 0, 0);
+      fresh = false;
+    }
+    // ---- one TraceStep level (engine.cpp:62-138)
+    bool done = false;
+    f3 L;
+    if (depth >= kMaxDepth) {
+      L = mk3(0, 0, 0);
+      done = true;
+    } else if (C.fast_render && depth > 1) {
+      L = mk3(1, 1, 1);
+      done = true;
+    } else {
+      segments++;
+      Hit h;
+      if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
+        if (depth == 1) lp0 = r.stop;
+        L = mk3(S.sky_r, S.sky_g, S.sky_b);
+        if (depth == 0) {
+          aov.normal = normalize(r.dir);
+          aov.id = S.sky_id;
+          aov.depth = C.z_far;
+        }
+        done = true;
+      } else {
+        if (depth == 1) lp0 = h.p;
+        const fs_material& m = S.materials[h.mat];
+        int32_t kind = m.kind;
+        f3 view = normalize(h.p - r.start);
+        f3 refl = mat_reflection(S, m, view, h.n, rng);
+        float c = fmaxf(0.0f, dot(h.n, refl));
+        float ds = 0.0f;
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
+          f3 hv = normalize(view * (float)-1.0 + refl);
+          ds = pow50(dot(hv, h.n));
+        }
+        lvl[depth * kBlock] = make_float2(c, ds);
+        if (depth < 4)
+          mats_lo |= (uint32_t)h.mat << (8 * depth);
+        else
+          mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
+        top = (int)depth;
+        if (depth == 0) {
+          p0 = h.p;
+          aov.normal = h.n;
+          aov.id = m.id;
+          aov.depth = length(r.start - h.p);
+        }
+        bool use = mat_will_use(m, refl, h.n);
+        Ray nr;  // engine.cpp:120-127
+        nr.start = h.p;
+        nr.stop = h.p + refl * C.z_far;
+        nr.dir = nr.stop - nr.start;
+        f3 off = refl * kStepOffset;
+        nr.start = nr.start + off;
+        nr.dir = nr.dir - off;
+        r = nr;
+        if (!use) {
+          L = mk3(0, 0, 0);
+          done = true;
+        } else {
+          depth++;
+        }
+      }
+    }
+    if (done) {  // ---- return path of the recursion + DisplayFrame::WritePixel
+      L = unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng);
+      f3 np = mean * (float)n + L;
+      float dv = (float)(++n);
+      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+      s++;
+      fresh = true;
+    }
+  }
+  F.color[3 * pix] = mean.x;
+  F.color[3 * pix + 1] = mean.y;
+  F.color[3 * pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * pix] = gamma8(mean.x);
+  F.display[3 * pix + 1] = gamma8(mean.y);
+  F.display[3 * pix + 2] = gamma8(mean.z);
+  if (P.spp) {
+    F.normal[3 * pix] = aov.normal.x;
+    F.normal[3 * pix + 1] = aov.normal.y;
+    F.normal[3 * pix + 2] = aov.normal.z;
+    F.depth[pix] = aov.depth;
+    F.material[pix] = aov.id;
+  }
+  if (COUNT) {
+    atomicAdd(&counters->samples, (unsigned long long)P.spp);
+    atomicAdd(&counters->segments, (unsigned long long)segments);
+    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+  }
+}
+
+
+// ============================================================================
+// Wavefront path tracer: extend (traversal only, high occupancy) and shade
+// (materials, RNG, next ray, accumulation) kernels over a compacted list of
+// live paths. One path slot per owned pixel; a slot walks its pixel's
+// samples in order, so the running mean is the reference's.
+// ============================================================================
+struct WfHit {
+  float t, u, v;
+  int32_t obj;    // -1: miss
+  uint32_t prim;  // mesh: global triangle; cuboid: face
+  uint32_t point; // 1: zero-length ray hit (point = ray start)
+  uint32_t pad0, pad1;
+};
+
+struct WfState {
+  uint32_t* pixel;
+  float4* ray0;  // start.xyz, dir.x
+  float4* ray1;  // dir.y, dir.z, stop.x, stop.y
+  float* ray2;   // stop.z
+  WfHit* hit;
+  uint64_t* rng;
+  uint4* path;   // depth, top, mats_lo, mats_hi
+  float4* p0;    // p0.xyz, lp0.x
+  float2* lp0;   // lp0.y, lp0.z
+  float2* lvl;   // kMaxDepth per slot
+  float4* acc;   // mean.xyz, count (bits)
+  uint32_t* samples;
+  float4* aov;   // normal.xyz, depth
+  uint64_t* aov_id;
+  uint32_t* list0;
+  uint32_t* list1;
+  uint32_t* count;  // [0], [1]: active counts
+};
+
+__device__ __forceinline__ Ray wf_load_ray(const WfState& W, uint32_t slot) {
+  float4 a = W.ray0[slot], b = W.ray1[slot];
+  Ray r;
+  r.start = mk3(a.x, a.y, a.z);
+  r.dir = mk3(a.w, b.x, b.y);
+  r.stop = mk3(b.z, b.w, W.ray2[slot]);
+  return r;
+}
+__device__ __forceinline__ void wf_store_ray(const WfState& W, uint32_t slot, const Ray& r) {
+  W.ray0[slot] = make_float4(r.start.x, r.start.y, r.start.z, r.dir.x);
+  W.ray1[slot] = make_float4(r.dir.y, r.dir.z, r.stop.x, r.stop.y);
+  W.ray2[slot] = r.stop.z;
+}
+
+struct MinHit {
+  float t, u, v;
+  int32_t obj;
+  uint32_t prim, point;
+};
+
+// BVH2 traversal of one mesh, closest-hit bookkeeping only (no point/normal).
+template <bool COUNT>
+__device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
+                                             MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
+  uint32_t w = root;
+  uint32_t sp = 0;
+  for (;;) {
+    if (!(w & kLeafBit)) {
+      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+      float4 X = q[0], Y = q[1], Z = q[2];
+      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
+      if (COUNT) tally.nodes++;
+      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+      bool h0, h1;
+      float t0, t1;
+      if (!zl) {
+        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
+        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
+        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
+        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
+        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
+        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
+        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
+        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
+        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
+        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
+        h0 = n0 <= f0;
+        h1 = n1 <= f1;
+        t0 = n0;
+        t1 = n1;
+      } else {
+        f3 s = r.start;
+        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
+        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
+        t0 = t1 = 0.0f;
+      }
+      if (h0 && h1) {
+        bool swap = t1 < t0;
+        stk[sp * kBlock] = swap ? Cw.x : Cw.y;
+        sp++;
+        w = swap ? Cw.y : Cw.x;
+        continue;
+      }
+      if (h0 || h1) {
+        w = h0 ? Cw.x : Cw.y;
+        continue;
+      }
+    } else {
+      uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
+      for (uint32_t i = 0; i < cnt; i++) {
+        uint32_t ti = first + i;
+        TriData T = load_tri(S.tris, ti);
+        if (COUNT) tally.tris++;
+        float t, u, v;
+        bool hit;
+        if (!zl) {
+          f3 p;
+          hit = ray_tri(T, r, t, p, u, v);
+        } else {
+          hit = point_in_tri(T, r.start, u, v);
+          t = 0.0f;
+        }
+        if (hit) {
+          bool better = t < h.t || (t == h.t && h.obj == oi && T.face < S.tris[h.prim].face);
+          if (better) {
+            h.t = t;
+            h.obj = oi;
+            h.prim = ti;
+            h.u = u;
+            h.v = v;
+            h.point = zl ? 1u : 0u;
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    sp--;
+    w = stk[sp * kBlock];
+  }
+}
+
+// Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
+template <bool COUNT>
+__device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
+                                                uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
+  h.t = 2.0f;
+  h.obj = -1;
+  h.prim = 0;
+  h.u = h.v = 0.0f;
+  h.point = 0;
+  bool zl = zero_len(r);
+  for (uint32_t oi = 0; oi < S.num_objects; ++oi) {
+    const DevObject* __restrict__ o = S.objects + oi;
+    int32_t kind = o->kind;
+    const float* d = o->d;
+    if (kind == FS_OBJ_MESH) {
+      if (!o->i2) continue;
+      if (!ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) continue;
+      traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+      continue;
+    }
+    if (zl) continue;
+    if (COUNT) tally.prims++;
+    float t;
+    f3 p, n;
+    if (kind == FS_OBJ_SPHERE) {
+      if (ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n) && t < h.t) {
+        h.t = t;
+        h.obj = (int32_t)oi;
+      }
+    } else if (kind == FS_OBJ_PLANE) {
+      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p) && t < h.t) {
+        h.t = t;
+        h.obj = (int32_t)oi;
+      }
+    } else if (kind == FS_OBJ_DISC) {
+      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p)) {
+        if (length(mk3(d[4], d[5], d[6]) - p) <= d[7] && t < h.t) {
+          h.t = t;
+          h.obj = (int32_t)oi;
+        }
+      }
+    } else if (kind == FS_OBJ_QUAD_ONWH) {
+      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p)) {
+        f3 ph = p - mk3(d[4], d[5], d[6]);
+        float td = dot(mk3(d[12], d[13], d[14]), ph);
+        float bd = dot(mk3(d[9], d[10], d[11]), ph);
+        if (!(fabsf(bd) > d[7] || fabsf(td) > d[8]) && t < h.t) {
+          h.t = t;
+          h.obj = (int32_t)oi;
+        }
+      }
+    } else if (kind == FS_OBJ_CUBOID) {
+      for (uint32_t i = 0; i < 6; i++) {
+        if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, t, p) && t < h.t) {
+          bool ok = true;
+          for (uint32_t j = 0; j < 6; j++) {
+            if (i / 2 != j / 2 && plane_dist(mk4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]), p) > 0.0f) {
+              ok = false;
+              break;
+            }
+          }
+          if (ok) {
+            h.t = t;
+            h.obj = (int32_t)oi;
+            h.prim = i;
+          }
+        }
+      }
+    }
+  }
+}
+
+// dense: one thread per slot in slot order (coherent, no list) while most
+// paths are alive; otherwise the compacted list `cur`.
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void wf_extend(DevScene S, WfState W, uint32_t cur, uint32_t dense, uint32_t spp,
+                                                     DevCounters* __restrict__ counters) {
+  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t slot;
+  if (dense) {
+    slot = i;
+    if (W.samples[slot] >= spp) return;
+  } else {
+    if (i >= W.count[cur]) return;
+    slot = (cur ? W.list1 : W.list0)[i];
+  }
+  Ray r = wf_load_ray(W, slot);
+  MinHit h;
+  Tally<COUNT> tally;
+  scene_trace_min<COUNT>(S, r, h, stk_all + threadIdx.x, tally);
+  WfHit o;
+  o.t = h.t;
+  o.u = h.u;
+  o.v = h.v;
+  o.obj = h.obj;
+  o.prim = h.prim;
+  o.point = h.point;
+  o.pad0 = o.pad1 = 0;
+  W.hit[slot] = o;
+  if (COUNT) {
+    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+  }
+}
+
+// Pixel of a slot: the same 8x8 micro-tile walk as render_kernel.
+__device__ __forceinline__ bool slot_pixel(const Launch& P, const DevFrame& F, uint32_t slot, uint32_t& x,
+                                           uint32_t& y) {
+  const uint32_t micro_per_side = P.tile_size / 8;
+  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t blk = slot / kBlock, lane = slot % kBlock;
+  const uint32_t owned = blk / micro_per_tile, micro = blk % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+  y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  return x < F.width && y < F.height;
+}
+
+__device__ __forceinline__ void wf_new_sample(const DevCamera& C, const Launch& P, const WfState& W, uint32_t slot,
+                                              uint32_t pix, uint32_t s, uint32_t width) {
+  uint64_t rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
+  Ray r = camera_ray(C, (float)(pix % width), (float)(pix / width), rng);
+  wf_store_ray(W, slot, r);
+  W.rng[slot] = rng;
+  W.path[slot] = make_uint4(0, 0xFFFFFFFFu, 0, 0);  // depth 0, top -1
+  W.p0[slot] = make_float4(0, 0, 0, 0);
+  W.lp0[slot] = make_float2(0, 0);
+}
+
+// Appends `keep` lanes' slots to list `nxt` with one atomic per wave.
+__device__ __forceinline__ void wf_append(const WfState& W, uint32_t nxt, bool keep, uint32_t slot,
+                                          bool write_list = true) {
+  uint64_t mask = __ballot(keep);
+  if (!mask) return;
+  uint32_t lane = threadIdx.x & 63u;
+  uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if ((int)lane == leader) base = atomicAdd(&W.count[nxt], (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  if (keep && write_list) (nxt ? W.list1 : W.list0)[base + rank] = slot;
+}
+
+// Compacts the live slots into list 0 (slot order within each wave).
+__global__ __launch_bounds__(kBlock) void wf_compact(WfState W, uint32_t slots, uint32_t spp) {
+  uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  bool keep = slot < slots && W.samples[slot] < spp;
+  wf_append(W, 0, keep, slot);
+}
+
+__global__ __launch_bounds__(kBlock) void wf_begin(DevCamera C, DevFrame F, Launch P, WfState W) {
+  uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t x, y;
+  bool keep = slot_pixel(P, F, slot, x, y) && P.spp > 0;
+  W.samples[slot] = P.spp;  // invalid slots stay "done"
+  if (keep) {
+    uint32_t pix = y * F.width + x;
+    W.pixel[slot] = pix;
+    W.acc[slot] = make_float4(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2],
+                              __uint_as_float(F.count[pix]));
+    W.samples[slot] = 0;
+    W.aov[slot] = make_float4(0, 0, 0, 0);
+    W.aov_id[slot] = 0;
+    wf_new_sample(C, P, W, slot, pix, 0, F.width);
+  }
+  wf_append(W, 0, keep, slot);
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void wf_shade(DevScene S, DevCamera C, DevFrame F, Launch P, WfState W,
+                                                    uint32_t cur, uint32_t dense, DevCounters* __restrict__ counters) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  bool keep = false;
+  uint32_t slot = 0;
+  bool live;
+  if (dense) {
+    slot = i;
+    live = W.samples[slot] < P.spp;
+  } else {
+    live = i < W.count[cur];
+    if (live) slot = (cur ? W.list1 : W.list0)[i];
+  }
+  if (live) {
+    Ray r = wf_load_ray(W, slot);
+    WfHit h = W.hit[slot];
+    uint4 path = W.path[slot];
+    uint32_t depth = path.x, mats_lo = path.z, mats_hi = path.w;
+    int top = (int)path.y;
+    uint64_t rng = W.rng[slot];
+    float2* lvl = W.lvl + (size_t)slot * kMaxDepth;
+    bool done = false;
+    f3 L = mk3(0, 0, 0);
+    if (h.obj < 0) {  // engine.cpp:88-102
+      if (depth == 1) W.lp0[slot] = make_float2(r.stop.y, r.stop.z), W.p0[slot].w = r.stop.x;
+      L = mk3(S.sky_r, S.sky_g, S.sky_b);
+      if (depth == 0) {
+        f3 nd = normalize(r.dir);
+        W.aov[slot] = make_float4(nd.x, nd.y, nd.z, C.z_far);
+        W.aov_id[slot] = S.sky_id;
+      }
+      done = true;
+    } else {
+      // Rebuild the hit exactly as the object tests produced it.
+      const DevObject* __restrict__ o = S.objects + h.obj;
+      const float* d = o->d;
+      f3 p = h.point ? r.start : r.start + r.dir * h.t;
+      f3 n;
+      if (o->kind == FS_OBJ_MESH) {
+        TriData T = load_tri(S.tris, h.prim);
+        n = xyz(T.pl);
+        if (o->i1) {  // mesh.cpp:289-298
+          const float4* nq = S.tri_normals + 3 * (size_t)h.prim;
+          float4 a = nq[0], b = nq[1], c = nq[2];
+          f3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(b.x, b.y, b.z), n2 = mk3(c.x, c.y, c.z);
+          n = n0 + (n1 - n0) * h.u + (n2 - n0) * h.v;
+        }
+      } else if (o->kind == FS_OBJ_SPHERE) {
+        n = normalize(p - mk3(d[0], d[1], d[2]));
+      } else if (o->kind == FS_OBJ_CUBOID) {
+        n = mk3(d[4 * h.prim], d[4 * h.prim + 1], d[4 * h.prim + 2]);
+      } else {
+        n = mk3(d[0], d[1], d[2]);
+      }
+      f4 cp = plane_np(n, p);  // scene.cpp:238-247
+      if (plane_dist(cp, r.start) < 0.0f) n = n * (float)-1.0;
+      if (depth == 1) W.lp0[slot] = make_float2(p.y, p.z), W.p0[slot].w = p.x;
+      int32_t mi = o->mat;
+      const fs_material& m = S.materials[mi];
+      int32_t kind = m.kind;
+      f3 view = normalize(p - r.start);
+      f3 refl = mat_reflection(S, m, view, n, rng);
+      float c = fmaxf(0.0f, dot(n, refl));
+      float ds = 0.0f;
+      if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {
+        f3 hv = normalize(view * (float)-1.0 + refl);
+        ds = pow50(dot(hv, n));
+      }
+      lvl[depth] = make_float2(c, ds);
+      if (depth < 4)
+        mats_lo |= (uint32_t)mi << (8 * depth);
+      else
+        mats_hi |= (uint32_t)mi << (8 * (depth - 4));
+      top = (int)depth;
+      if (depth == 0) {
+        W.p0[slot] = make_float4(p.x, p.y, p.z, 0.0f);
+        W.aov[slot] = make_float4(n.x, n.y, n.z, length(r.start - p));
+        W.aov_id[slot] = m.id;
+      }
+      bool use = mat_will_use(m, refl, n);
+      Ray nr;  // engine.cpp:120-127
+      nr.start = p;
+      nr.stop = p + refl * C.z_far;
+      nr.dir = nr.stop - nr.start;
+      f3 off = refl * kStepOffset;
+      nr.start = nr.start + off;
+      nr.dir = nr.dir - off;
+      if (!use) {
+        done = true;
+      } else {
+        depth++;
+        if (depth >= kMaxDepth) {  // engine.cpp:62-64
+          done = true;
+        } else if (C.fast_render && depth > 1) {  // engine.cpp:68-70
+          L = mk3(1, 1, 1);
+          done = true;
+        } else {
+          wf_store_ray(W, slot, nr);
+        }
+      }
+    }
+    if (done) {
+      float4 pa = W.p0[slot];
+      float2 pb = W.lp0[slot];
+      L = unwind(S, L, top, mats_lo, mats_hi, lvl, mk3(pa.x, pa.y, pa.z), mk3(pa.w, pb.x, pb.y), rng, 1);
+      float4 acc = W.acc[slot];
+      uint32_t n = __float_as_uint(acc.w);
+      f3 np = mk3(acc.x, acc.y, acc.z) * (float)n + L;
+      float dv = (float)(++n);
+      f3 mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+      uint32_t s = W.samples[slot] + 1;
+      W.samples[slot] = s;
+      if (s < P.spp) {
+        W.acc[slot] = make_float4(mean.x, mean.y, mean.z, __uint_as_float(n));
+        wf_new_sample(C, P, W, slot, W.pixel[slot], s, F.width);
+        keep = true;
+      } else {  // all samples of this pixel done: write the DisplayFrame
+        size_t pix = W.pixel[slot];
+        F.color[3 * pix] = mean.x;
+        F.color[3 * pix + 1] = mean.y;
+        F.color[3 * pix + 2] = mean.z;
+        F.count[pix] = n;
+        F.display[3 * pix] = gamma8(mean.x);
+        F.display[3 * pix + 1] = gamma8(mean.y);
+        F.display[3 * pix + 2] = gamma8(mean.z);
+        float4 av = W.aov[slot];
+        F.normal[3 * pix] = av.x;
+        F.normal[3 * pix + 1] = av.y;
+        F.normal[3 * pix + 2] = av.z;
+        F.depth[pix] = av.w;
+        F.material[pix] = W.aov_id[slot];
+      }
+    } else {
+      W.path[slot] = make_uint4(depth, (uint32_t)top, mats_lo, mats_hi);
+      W.rng[slot] = rng;
+      keep = true;
+    }
+    if (COUNT) {
+      atomicAdd(&counters->segments, 1ull);
+      if (done) atomicAdd(&counters->samples, 1ull);
+    }
+  }
+  wf_append(W, cur ^ 1u, keep, slot, !dense);
 }
 
 // ---- multi-GPU packing: 10 words per pixel (colour, count, normal, depth, id)
@@ -792,6 +1485,9 @@ struct fs_context {
   float last_ms = 0.0f;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  DevBuf wf;              // wavefront path state (slots x ~250 B)
+  uint32_t wf_slots = 0;
+  uint32_t* host_count = nullptr;  // pinned
 };
 
 struct fs_frame {
@@ -859,6 +1555,42 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
   b.z_far = c->z_far;
   b.fast_render = c->fast_render;
   return b;
+}
+
+// Carves the wavefront state for `slots` paths out of one allocation.
+int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
+  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 16 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4;
+  size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
+  if (ctx->wf.bytes < bytes) {
+    int rc = ensure(&ctx->wf, bytes);
+    if (rc) return rc;
+  }
+  char* p = (char*)ctx->wf.p;
+  auto take = [&](size_t n) {
+    char* q = p;
+    p += (n + 255) & ~(size_t)255;
+    return q;
+  };
+  W->count = (uint32_t*)take(64);
+  W->pixel = (uint32_t*)take(4ull * slots);
+  W->ray0 = (float4*)take(16ull * slots);
+  W->ray1 = (float4*)take(16ull * slots);
+  W->ray2 = (float*)take(4ull * slots);
+  W->hit = (dev::WfHit*)take(sizeof(dev::WfHit) * (size_t)slots);
+  W->rng = (uint64_t*)take(8ull * slots);
+  W->path = (uint4*)take(16ull * slots);
+  W->p0 = (float4*)take(16ull * slots);
+  W->lp0 = (float2*)take(8ull * slots);
+  W->lvl = (float2*)take(8ull * kMaxDepth * slots);
+  W->acc = (float4*)take(16ull * slots);
+  W->samples = (uint32_t*)take(4ull * slots);
+  W->aov = (float4*)take(16ull * slots);
+  W->aov_id = (uint64_t*)take(8ull * slots);
+  W->list0 = (uint32_t*)take(4ull * slots);
+  W->list1 = (uint32_t*)take(4ull * slots);
+  if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "wavefront state overflow");
+  if (!ctx->host_count) FS_HIP(hipHostMalloc((void**)&ctx->host_count, 16, hipHostMallocDefault));
+  return FS_OK;
 }
 
 size_t plane_bytes(int plane, size_t pixels) {
@@ -952,6 +1684,8 @@ int fs_destroy(fs_context* ctx) {
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->materials, &ctx->table,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
     b->release();
+  ctx->wf.release();
+  if (ctx->host_count) (void)hipHostFree(ctx->host_count);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1112,16 +1846,70 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // Long renders are split into launches of at most `chunk` samples per
   // pixel; the running mean lives in the frame, so the result is identical.
   const uint32_t chunk = 32;
+  // FS_KERNEL=1 selects the sample-lockstep kernel (A/B); default: path regeneration.
+  const int variant = std::getenv("FS_KERNEL") ? std::atoi(std::getenv("FS_KERNEL")) : 4;
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+  if (variant == 5 && blocks && params->spp) {
+    // Wavefront: begin -> (extend, shade)* until no path is alive.
+    dev::WfState W;
+    uint32_t slots = (uint32_t)(blocks * kBlock);
+    if ((rc = wf_state(ctx, slots, &W))) return rc;
+    L.sample_base = params->sample_base;
+    L.spp = params->spp;
+    FS_HIP(hipMemsetAsync(W.count, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(dev::wf_begin, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, C, F, L, W);
+    FS_HIP(hipGetLastError());
+    auto ext = count ? dev::wf_extend<true> : dev::wf_extend<false>;
+    auto shd = count ? dev::wf_shade<true> : dev::wf_shade<false>;
+    DevCounters* dc = (DevCounters*)ctx->counters.p;
+    uint32_t grid = (uint32_t)blocks;
+    auto read_count = [&](uint32_t which, uint32_t* out) -> int {
+      FS_HIP(hipMemcpyAsync(ctx->host_count, W.count + which, 4, hipMemcpyDeviceToHost, ctx->stream));
+      FS_HIP(hipStreamSynchronize(ctx->stream));
+      *out = *ctx->host_count;
+      return FS_OK;
+    };
+    // Dense phase: every slot in slot order until fewer than half are alive.
+    uint32_t live = slots;
+    for (uint32_t it = 1;; it++) {
+      FS_HIP(hipMemsetAsync(W.count + 1, 0, 4, ctx->stream));
+      hipLaunchKernelGGL(ext, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, W, 0u, 1u, L.spp, dc);
+      hipLaunchKernelGGL(shd, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, W, 0u, 1u, dc);
+      FS_HIP(hipGetLastError());
+      if (it % 8 == 0) {
+        if ((rc = read_count(1, &live))) return rc;
+        if (live == 0 || live < slots / 2) break;
+      }
+    }
+    // Sparse phase: compacted lists (ballot + one atomic per wave).
+    uint32_t cur = 0;
+    if (live) {
+      FS_HIP(hipMemsetAsync(W.count, 0, 4, ctx->stream));
+      hipLaunchKernelGGL(dev::wf_compact, dim3(grid), dim3(kBlock), 0, ctx->stream, W, slots, L.spp);
+      FS_HIP(hipGetLastError());
+      if ((rc = read_count(0, &live))) return rc;
+    }
+    for (uint32_t it = 1; live; it++) {
+      uint32_t g = (live + kBlock - 1) / kBlock;
+      FS_HIP(hipMemsetAsync(W.count + (cur ^ 1u), 0, 4, ctx->stream));
+      hipLaunchKernelGGL(ext, dim3(g), dim3(kBlock), 0, ctx->stream, ctx->scene, W, cur, 0u, L.spp, dc);
+      hipLaunchKernelGGL(shd, dim3(g), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, W, cur, 0u, dc);
+      FS_HIP(hipGetLastError());
+      cur ^= 1u;
+      if ((rc = read_count(cur, &live))) return rc;
+    }
+    FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return FS_OK;
+  }
   for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
-    if (count)
-      hipLaunchKernelGGL(dev::render_kernel<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream,
-                         ctx->scene, C, F, L, (DevCounters*)ctx->counters.p);
-    else
-      hipLaunchKernelGGL(dev::render_kernel<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream,
-                         ctx->scene, C, F, L, (DevCounters*)ctx->counters.p);
+    auto kern = count ? dev::render_kernel_regen<true, 2> : dev::render_kernel_regen<false, 2>;
+    if (variant == 1) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
+    if (variant == 3) kern = count ? dev::render_kernel_regen<true, 3> : dev::render_kernel_regen<false, 3>;
+    if (variant == 4) kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
+                       (DevCounters*)ctx->counters.p);
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));

@@ -120,6 +120,38 @@ struct Prim {
   uint32_t face;
 };
 
+// Fills the ray-independent part of the reference triangle test.
+void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
+  f3 v0 = p1 - p0, v1 = p2 - p0;
+  float ax = std::fabs(pl.x), ay = std::fabs(pl.y), az = std::fabs(pl.z);
+  uint32_t axis;
+  if (ax >= ay)
+    axis = ax >= az ? 0u : 2u;
+  else
+    axis = ay >= az ? 1u : 2u;
+  if (axis == 0) v0.x = v1.x = 0;
+  if (axis == 1) v0.y = v1.y = 0;
+  if (axis == 2) v0.z = v1.z = 0;
+  t->p1[0] = p0.x;
+  t->p1[1] = p0.y;
+  t->p1[2] = p0.z;
+  t->v0[0] = v0.x;
+  t->v0[1] = v0.y;
+  t->v0[2] = v0.z;
+  t->v1[0] = v1.x;
+  t->v1[1] = v1.y;
+  t->v1[2] = v1.z;
+  t->d00 = dot(v0, v0);
+  t->d01 = dot(v0, v1);
+  t->d11 = dot(v1, v1);
+  t->inv = 1 / (t->d00 * t->d11 - t->d01 * t->d01);
+  t->axis = axis;
+  t->plane[0] = pl.x;
+  t->plane[1] = pl.y;
+  t->plane[2] = pl.z;
+  t->plane[3] = pl.w;
+}
+
 constexpr int kBins = 16;
 constexpr uint32_t kLeafTarget = 4;
 
@@ -141,7 +173,7 @@ class BvhBuilder {
       split_into(root, 0, (uint32_t)prims.size(), 1);
     }
     *max_depth = std::max(*max_depth, max_depth_);
-    return root;
+    return overflow_ ? 0xFFFFFFFFu : root;
   }
 
  private:
@@ -185,6 +217,7 @@ class BvhBuilder {
     n.child[slot] = word;
   }
   uint32_t make_leaf(uint32_t b, uint32_t e) {
+    if (e - b > kMaxLeafCount) overflow_ = true;  // cannot be encoded: reported by build()
     uint32_t start = (uint32_t)tris_->size();
     for (uint32_t i = b; i < e; i++) {
       uint32_t f = (*prims_)[i].face;
@@ -291,6 +324,7 @@ class BvhBuilder {
   const std::vector<float>* mesh_normals_;
   std::vector<Prim>* prims_ = nullptr;
   uint32_t max_depth_ = 0;
+  bool overflow_ = false;
 };
 
 void cube_planes(const f3* v, float* d) {  // volume.cpp:234-247
@@ -491,6 +525,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     mesh_out[mi].normals = nn > 0;
     uint32_t nt = m.texcoords ? m.num_texcoords : 0;
     std::vector<DevTri> mtris(m.num_triangles);
+    std::vector<float> corner_pos(need ? 9 * (size_t)m.num_triangles : 0);
     std::vector<float> mnormals;
     if (any_normals) mnormals.assign(12 * (size_t)m.num_triangles, 0.0f);
     for (uint32_t f = 0; f < m.num_triangles; f++) {
@@ -518,10 +553,10 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       t.face = f;
       if (need) {
         f3 p0 = verts[vi[0]], p1 = verts[vi[1]], p2 = verts[vi[2]];
-        put3(t.p1, p0);
-        put3(t.p2, p1);
-        put3(t.p3, p2);
-        put4(t.plane, plane_np(calc_normal(p0, p1, p2), p0));  // mesh.cpp:136-146
+        fill_tri(&t, p0, p1, p2, plane_np(calc_normal(p0, p1, p2), p0));  // mesh.cpp:136-146
+        for (int k = 0; k < 3; k++) corner_pos[9 * (size_t)f + 3 * k + 0] = verts[vi[k]].x;
+        for (int k = 0; k < 3; k++) corner_pos[9 * (size_t)f + 3 * k + 1] = verts[vi[k]].y;
+        for (int k = 0; k < 3; k++) corner_pos[9 * (size_t)f + 3 * k + 2] = verts[vi[k]].z;
       }
       if (nn)
         for (int k = 0; k < 3; k++) put3(&mnormals[12 * (size_t)f + 4 * k], normals[ni[k]]);
@@ -535,15 +570,19 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     std::vector<Prim> prims(m.num_triangles);
     for (uint32_t f = 0; f < m.num_triangles; f++) {
       Prim& p = prims[f];
-      p.box.grow(mtris[f].p1);
-      p.box.grow(mtris[f].p2);
-      p.box.grow(mtris[f].p3);
+      p.box.grow(&corner_pos[9 * (size_t)f]);
+      p.box.grow(&corner_pos[9 * (size_t)f + 3]);
+      p.box.grow(&corner_pos[9 * (size_t)f + 6]);
       for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
       p.face = f;
     }
     for (DevTri& t : mtris) t.mesh_obj = mi;
     BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &mtris, &mnormals);
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
+    if (mesh_out[mi].root == 0xFFFFFFFFu) {
+      *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
+      return FS_ERR_INVALID;
+    }
   }
 
   S.objects.resize(d->num_objects);

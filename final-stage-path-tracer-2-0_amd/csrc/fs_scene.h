@@ -46,21 +46,28 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kMaxLeafCount = 127;
 constexpr uint32_t kMaxTriangles = 1u << 24;
-constexpr uint32_t kTraversalStack = 32;  // BVH depth bound (builder enforces)
+constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
 
-// Triangle record, 64 B: the reference test operands (intersect.cpp:357-419)
-// — the three corners in the reference's reversed winding plus the
-// precomputed face plane (mesh.cpp:136-146) — and the face index (tie-break).
+// Triangle record, 80 B: the operands of the reference test
+// (intersect.cpp:357-419) with every ray-independent term precomputed on the
+// host by the same float operations: p1, the planar-mapped edges v0 = p2-p1
+// and v1 = p3-p1 (dominant plane axis zeroed, intersect.cpp:96-129), their
+// dot products and 1/(d00*d11 - d01*d01) (:168-173), the face plane
+// (mesh.cpp:136-146, reversed winding) and the face index (tie-break).
 struct DevTri {
   float p1[3];
   uint32_t face;
-  float p2[3];
+  float v0[3];
+  float d00;
+  float v1[3];
+  float d01;
+  float d11;
+  float inv;
+  uint32_t axis;  // zeroed component of the planar map (0=x, 1=y, 2=z)
   uint32_t mesh_obj;
-  float p3[3];
-  float pad;
   float plane[4];
 };
-static_assert(sizeof(DevTri) == 64, "DevTri layout");
+static_assert(sizeof(DevTri) == 80, "DevTri layout");
 
 struct PreparedScene {
   std::vector<DevObject> objects;

@@ -1,0 +1,55 @@
+"""Interleaved A/B of kernel variants (FS_KERNEL env) in one process.
+usage: python tools/perf_ab.py variants scenes [spp] [rounds]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "final-stage-path-tracer-2-0_amd"))
+import numpy as np  # noqa: E402
+
+import fsamd  # noqa: E402
+import scenes  # noqa: E402
+
+
+def main():
+    variants = sys.argv[1].split(",")
+    names = sys.argv[2].split(",")
+    spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    W, H = 1920, 1080
+    tmp = os.path.join(ROOT, "gpurun_out", "scenes")
+    for name in names:
+        p = scenes.write(name, os.path.join(tmp, name))
+        fsamd.reset_main_rng()
+        s = fsamd.HostScene.load(p)
+        fsamd.initialize_materials()
+        r = fsamd.Renderer(0)
+        r.upload(s)
+        cam = s.camera(0)
+        f = r.frame(W, H)
+        res = {v: [] for v in variants}
+        ref = None
+        for rd in range(rounds + 1):
+            for v in variants:
+                os.environ["FS_KERNEL"] = v
+                f.reset()
+                r.render(cam, f, spp=spp)
+                ms = r.last_render_ms()
+                if rd:
+                    res[v].append(ms)
+                img = f.read(fsamd.PLANE_COLOR)
+                if ref is None:
+                    ref = img
+                elif not np.array_equal(img, ref):
+                    print(f"  !! variant {v} output differs from variant {variants[0]}", flush=True)
+        for v in variants:
+            ms = np.median(res[v])
+            print(f"{name} variant {v}: median {ms:.1f} ms  {W*H*spp/ms/1e3:.1f} Msamples/s  (min {min(res[v]):.1f})",
+                  flush=True)
+        f.close()
+        r.close()
+
+
+if __name__ == "__main__":
+    main()
