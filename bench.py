@@ -37,10 +37,10 @@ WORKLOADS = {
     "c3": "~250k-triangle procedural atrium (BASELINE configs[2]) at 1920x1080, 1024 spp",
 }
 # Algorithmic bytes per unit of work, from the device SoA record
-# sizes: BVH node 64 B, triangle 64 B, analytic object record 128 B, per
+# sizes: BVH node 64 B, triangle 80 B, analytic object record 128 B, per
 # segment one material record (76 B) + one normal-table entry (16 B); per
 # sample 12 B of radiance.
-S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
+S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 80, 128, 92, 12
 
 
 def parse():
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--cpu-spp", type=int, default=1, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-tile-stride", type=int, default=4, help="CPU sample renders 1/stride of the tiles")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -160,7 +160,7 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "render_kernel_regen<false, 4>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "kernel": "render_kernel_lean<false, 6, true>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "bytes_per_sample": round(bytes_per_sample, 1),
                 "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
                 "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),

@@ -8,10 +8,12 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "fs_kernels.h"
@@ -576,12 +578,20 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
 // engine.cpp:210-244. Returns the TraceResult colour.
 // Backward pass: Material::Sample in the order the TraceStep recursion
 // returns (engine.cpp:141-156); L enters as the radiance of level `top`+1.
+// base + a 32-bit byte offset: lets the compiler use the SGPR-base + 32-bit
+// VGPR-offset addressing form instead of keeping a 64-bit pointer per lane.
+template <class T>
+__device__ __forceinline__ T* at_byte(T* base, uint32_t off) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
+}
+
 __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t mats_lo, uint32_t mats_hi,
                                      const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
-                                     int stride = kBlock) {
+                                     int stride = kBlock, uint32_t lane = 0) {
   for (int k = top; k >= 0; --k) {
     const fs_material& m = S.materials[mat_of(mats_lo, mats_hi, k)];
-    float2 cs = lvl[k * stride];
+    float2 cs = *at_byte(lvl, ((uint32_t)k * (uint32_t)stride + lane) * 8u);
     f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
     switch (m.kind) {
       case FS_MAT_LIGHT:
@@ -1053,10 +1063,144 @@ __device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, i
   }
 }
 
-// Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
+// The same traversal restructured as while-while with postponed leaves
+// (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking
+// inner nodes until every active lane holds a leaf, then the wave tests the
+// parked leaves together. Inner-node and triangle code no longer interleave
+// per iteration. The closest hit is a total order on (t, face), so the test
+// order does not change the result.
 template <bool COUNT>
+__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl, MinHit& h,
+                                          Tally<COUNT>& tally) {
+  uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
+  for (uint32_t i = 0; i < cnt; i++) {
+    uint32_t ti = first + i;
+    TriData T = load_tri(S.tris, ti);
+    if (COUNT) tally.tris++;
+    float t, u, v;
+    bool hit;
+    if (!zl) {
+      f3 p;
+      hit = ray_tri(T, r, t, p, u, v);
+    } else {
+      hit = point_in_tri(T, r.start, u, v);
+      t = 0.0f;
+    }
+    if (hit) {
+      bool better = t < h.t || (t == h.t && h.obj == oi && T.face < S.tris[h.prim].face);
+      if (better) {
+        h.t = t;
+        h.obj = oi;
+        h.prim = ti;
+        h.u = u;
+        h.v = v;
+        h.point = zl ? 1u : 0u;
+      }
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
+                                            MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
+  constexpr uint32_t kNone = 0x7FFFFFFFu;  // empty-stack sentinel (no leaf bit, never a node index)
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
+  uint32_t w = root, leaf = 0, sp = 0;
+  while (w != kNone || leaf) {
+    while (!(w & kLeafBit) && w != kNone) {
+      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+      float4 X = q[0], Y = q[1], Z = q[2];
+      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
+      if (COUNT) tally.nodes++;
+      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+      bool h0, h1;
+      float t0, t1;
+      if (!zl) {
+        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
+        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
+        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
+        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
+        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
+        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
+        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
+        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
+        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
+        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
+        h0 = n0 <= f0;
+        h1 = n1 <= f1;
+        t0 = n0;
+        t1 = n1;
+      } else {
+        f3 s = r.start;
+        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
+        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
+        t0 = t1 = 0.0f;
+      }
+      if (h0 && h1) {
+        bool swap = t1 < t0;
+        stk[sp * kBlock] = swap ? Cw.x : Cw.y;
+        sp++;
+        w = swap ? Cw.y : Cw.x;
+      } else if (h0 || h1) {
+        w = h0 ? Cw.x : Cw.y;
+      } else {
+        w = sp ? stk[--sp * kBlock] : kNone;
+      }
+      if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
+        leaf = w;
+        w = sp ? stk[--sp * kBlock] : kNone;
+      }
+      if (__ballot(leaf == 0) == 0) break;  // every active lane holds a leaf
+    }
+    while (leaf) {
+      test_leaf<COUNT>(S, leaf, oi, r, zl, h, tally);
+      leaf = 0;
+      if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
+        leaf = w;
+        w = sp ? stk[--sp * kBlock] : kNone;
+      }
+    }
+  }
+}
+
+// Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
+// Conservative segment-vs-box cull for analytic objects (not a reference
+// test): the slab interval uses v_rcp and the same t margins as the BVH
+// traversal, against a box padded on the host (fs_scene.cpp). A segment that
+// can produce a hit with t < best always passes.
+__device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, const float* __restrict__ b) {
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+  float a0 = (b[0] - r.start.x) * ix, a1 = (b[3] - r.start.x) * ix;
+  float c0 = (b[1] - r.start.y) * iy, c1 = (b[4] - r.start.y) * iy;
+  float e0 = (b[2] - r.start.z) * iz, e1 = (b[5] - r.start.z) * iz;
+  float tn = fmaxf(fmaxf(fminf(a0, a1), fminf(c0, c1)), fmaxf(fminf(e0, e1), -1e-6f));
+  float tf = fminf(fminf(fmaxf(a0, a1), fmaxf(c0, c1)), fminf(fmaxf(e0, e1), fminf(best, 1.0f) * 1.000002f + 1e-7f));
+  return tn <= tf;
+}
+
+#ifdef FS_PHASE_PROF
+struct PhaseAcc {
+  uint64_t cull = 0, trav = 0, prim = 0;
+};
+#define FS_TICK() __builtin_readcyclecounter()
+#else
+struct PhaseAcc {};
+#define FS_TICK() 0ull
+#endif
+
+template <bool COUNT, bool WW = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
-                                                uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
+                                                uint32_t* __restrict__ stk, Tally<COUNT>& tally,
+                                                PhaseAcc& pa) {
   h.t = 2.0f;
   h.obj = -1;
   h.prim = 0;
@@ -1069,10 +1213,28 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     const float* d = o->d;
     if (kind == FS_OBJ_MESH) {
       if (!o->i2) continue;
-      if (!ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) continue;
-      traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+      uint64_t t0 = FS_TICK();
+      bool visit = ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
+      uint64_t t1 = FS_TICK();
+      if (visit) {
+        if (WW)
+          traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+        else
+          traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+      }
+#ifdef FS_PHASE_PROF
+      uint64_t t2 = FS_TICK();
+      pa.cull += t1 - t0;
+      pa.trav += t2 - t1;
+#else
+      (void)t0;
+      (void)t1;
+#endif
       continue;
     }
+#ifdef FS_PHASE_PROF
+    uint64_t tp0 = FS_TICK();
+#endif
     if (zl) continue;
     if (COUNT) tally.prims++;
     float t;
@@ -1105,6 +1267,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         }
       }
     } else if (kind == FS_OBJ_CUBOID) {
+      if (!seg_box_cull(r, h.t, d + 24)) continue;
       for (uint32_t i = 0; i < 6; i++) {
         if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, t, p) && t < h.t) {
           bool ok = true;
@@ -1122,6 +1285,9 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         }
       }
     }
+#ifdef FS_PHASE_PROF
+    pa.prim += FS_TICK() - tp0;
+#endif
   }
 }
 
@@ -1143,7 +1309,8 @@ __global__ __launch_bounds__(kBlock) void wf_extend(DevScene S, WfState W, uint3
   Ray r = wf_load_ray(W, slot);
   MinHit h;
   Tally<COUNT> tally;
-  scene_trace_min<COUNT>(S, r, h, stk_all + threadIdx.x, tally);
+  PhaseAcc pa;
+  scene_trace_min<COUNT>(S, r, h, stk_all + threadIdx.x, tally, pa);
   WfHit o;
   o.t = h.t;
   o.u = h.u;
@@ -1370,6 +1537,225 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene S, DevCamera C, DevF
   wf_append(W, cur ^ 1u, keep, slot, !dense);
 }
 
+
+// Rebuilds the hit point/normal of a MinHit exactly as the object tests
+// produced them (object.cpp, mesh.cpp:289-298) and applies the back-face
+// flip of Scene::Trace (scene.cpp:238-247).
+__device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, const MinHit& h, f3& p, f3& n,
+                                            int32_t& mat) {
+  const DevObject* __restrict__ o = S.objects + h.obj;
+  const float* d = o->d;
+  p = h.point ? r.start : r.start + r.dir * h.t;
+  int32_t kind = o->kind;
+  if (kind == FS_OBJ_MESH) {
+    const float4* q = reinterpret_cast<const float4*>(S.tris + h.prim);
+    float4 pl = q[4];
+    n = mk3(pl.x, pl.y, pl.z);
+    if (o->i1) {
+      const float4* nq = S.tri_normals + 3 * (size_t)h.prim;
+      float4 a = nq[0], b = nq[1], c = nq[2];
+      f3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(b.x, b.y, b.z), n2 = mk3(c.x, c.y, c.z);
+      n = n0 + (n1 - n0) * h.u + (n2 - n0) * h.v;
+    }
+  } else if (kind == FS_OBJ_SPHERE) {
+    n = normalize(p - mk3(d[0], d[1], d[2]));
+  } else if (kind == FS_OBJ_CUBOID) {
+    n = mk3(d[4 * h.prim], d[4 * h.prim + 1], d[4 * h.prim + 2]);
+  } else {
+    n = mk3(d[0], d[1], d[2]);
+  }
+  f4 cp = plane_np(n, p);
+  if (plane_dist(cp, r.start) < 0.0f) n = n * (float)-1.0;
+  mat = o->mat;
+}
+
+// Path regeneration with a lean register footprint: the closest-hit query
+// keeps only (t, object, primitive, u, v); the per-bounce shading scalars
+// and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
+// AOVs go straight to the frame. Same outputs as render_kernel_regen.
+template <bool COUNT, int WAVES, bool WW = false>
+__global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
+                                                                     float2* __restrict__ lvl_all,
+                                                                     float4* __restrict__ anchor_all,
+                                                                     DevCounters* __restrict__ counters) {
+  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  const uint32_t lane = threadIdx.x;
+  uint32_t* stk = stk_all + lane;
+  // Scratch rows, depth-major per wave ([level][lane]) so a wave's store is
+  // one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
+  float2* lvl = lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
+  float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
+  const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
+
+  uint32_t x, y;
+  {
+    const uint32_t micro_per_side = P.tile_size / 8;
+    const uint32_t micro_per_tile = micro_per_side * micro_per_side;
+    const uint32_t owned = blockIdx.x / micro_per_tile, micro = blockIdx.x % micro_per_tile;
+    const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+    const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+    y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  }
+  if (x >= F.width || y >= F.height) return;
+  const uint32_t pix = y * F.width + x;
+  f3 mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
+  uint32_t n = F.count[pix];
+  Tally<COUNT> tally;
+  uint32_t segments = 0;
+
+  uint32_t s = 0;
+  uint64_t rng = 0;
+  Ray r;
+  uint32_t depth = 0, mats_lo = 0, mats_hi = 0;
+  int top = -1;
+  bool fresh = true;
+#ifdef FS_PHASE_PROF
+  uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tk = __builtin_readcyclecounter(), t_begin = tk;
+#define FS_PHASE(i)                                 \
+  do {                                              \
+    uint64_t now_ = __builtin_readcyclecounter();   \
+    ph[i] += now_ - tk;                             \
+    tk = now_;                                      \
+  } while (0)
+#else
+#define FS_PHASE(i) \
+  do {              \
+  } while (0)
+#endif
+  while (s < P.spp) {
+    FS_PHASE(0);
+    if (fresh) {
+      rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
+      r = camera_ray(C, (float)x, (float)y, rng);
+      depth = 0;
+      mats_lo = mats_hi = 0;
+      top = -1;
+      *at_byte(anchor, a0_off) = make_float4(0, 0, 0, 0);
+      *at_byte(anchor, a1_off) = make_float4(0, 0, 0, 0);
+      fresh = false;
+    }
+    FS_PHASE(1);
+    bool done = false;
+    f3 L = mk3(0, 0, 0);
+    if (depth >= kMaxDepth) {
+      done = true;
+    } else if (C.fast_render && depth > 1) {
+      L = mk3(1, 1, 1);
+      done = true;
+    } else {
+      segments++;
+      MinHit h;
+#ifdef FS_PHASE_PROF
+      PhaseAcc pa;
+      scene_trace_min<COUNT, WW>(S, r, h, stk, tally, pa);
+      ph[5] += pa.cull;
+      ph[6] += pa.trav;
+      ph[7] += pa.prim;
+#else
+      PhaseAcc pa;
+      scene_trace_min<COUNT, WW>(S, r, h, stk, tally, pa);
+#endif
+      FS_PHASE(2);
+      if (h.obj < 0) {
+        if (depth == 1) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
+        L = mk3(S.sky_r, S.sky_g, S.sky_b);
+        if (depth == 0) {
+          f3 nd = normalize(r.dir);
+          at_byte(F.normal, pix * 12u)[0] = nd.x;
+          at_byte(F.normal, pix * 12u)[1] = nd.y;
+          at_byte(F.normal, pix * 12u)[2] = nd.z;
+          *at_byte(F.depth, pix * 4u) = C.z_far;
+          *at_byte(F.material, pix * 8u) = S.sky_id;
+        }
+        done = true;
+      } else {
+        f3 p, nn;
+        int32_t mi;
+        rebuild_hit(S, r, h, p, nn, mi);
+        if (depth == 1) *at_byte(anchor, a1_off) = make_float4(p.x, p.y, p.z, 0);
+        const fs_material& m = S.materials[mi];
+        int32_t kind = m.kind;
+        f3 view = normalize(p - r.start);
+        f3 refl = mat_reflection(S, m, view, nn, rng);
+        float c = fmaxf(0.0f, dot(nn, refl));
+        float ds = 0.0f;
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {
+          f3 hv = normalize(view * (float)-1.0 + refl);
+          ds = pow50(dot(hv, nn));
+        }
+        *at_byte(lvl, (depth * kBlock + lane) * 8u) = make_float2(c, ds);
+        if (depth < 4)
+          mats_lo |= (uint32_t)mi << (8 * depth);
+        else
+          mats_hi |= (uint32_t)mi << (8 * (depth - 4));
+        top = (int)depth;
+        if (depth == 0) {
+          *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
+          at_byte(F.normal, pix * 12u)[0] = nn.x;
+          at_byte(F.normal, pix * 12u)[1] = nn.y;
+          at_byte(F.normal, pix * 12u)[2] = nn.z;
+          *at_byte(F.depth, pix * 4u) = length(r.start - p);
+          *at_byte(F.material, pix * 8u) = m.id;
+        }
+        bool use = mat_will_use(m, refl, nn);
+        Ray nr;
+        nr.start = p;
+        nr.stop = p + refl * C.z_far;
+        nr.dir = nr.stop - nr.start;
+        f3 off = refl * kStepOffset;
+        nr.start = nr.start + off;
+        nr.dir = nr.dir - off;
+        r = nr;
+        if (!use)
+          done = true;
+        else
+          depth++;
+      }
+    }
+    FS_PHASE(3);
+    if (done) {
+      f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
+      if (top >= 0 && S.materials[mats_lo & 0xFFu].kind == FS_MAT_FOG) {
+        float4 a = *at_byte(anchor, a0_off), b = *at_byte(anchor, a1_off);
+        p0 = mk3(a.x, a.y, a.z);
+        lp0 = mk3(b.x, b.y, b.z);
+      }
+      L = unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane);
+      f3 np = mean * (float)n + L;
+      float dv = (float)(++n);
+      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+      s++;
+      fresh = true;
+    }
+    FS_PHASE(4);
+#ifdef FS_PHASE_PROF
+    ph[8]++;
+#endif
+  }
+#ifdef FS_PHASE_PROF
+  ph[9] = __builtin_readcyclecounter() - t_begin;
+  if (lane == 0)
+    for (int i = 0; i < 10; i++) atomicAdd(&counters->phase[i], (unsigned long long)ph[i]);
+#endif
+#undef FS_PHASE
+  F.color[3 * (size_t)pix] = mean.x;
+  F.color[3 * (size_t)pix + 1] = mean.y;
+  F.color[3 * (size_t)pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * (size_t)pix] = gamma8(mean.x);
+  F.display[3 * (size_t)pix + 1] = gamma8(mean.y);
+  F.display[3 * (size_t)pix + 2] = gamma8(mean.z);
+  if (COUNT) {
+    atomicAdd(&counters->samples, (unsigned long long)P.spp);
+    atomicAdd(&counters->segments, (unsigned long long)segments);
+    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+  }
+}
+
 // ---- multi-GPU packing: 10 words per pixel (colour, count, normal, depth, id)
 constexpr uint32_t kPackWords = 10;
 
@@ -1559,7 +1945,7 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 
 // Carves the wavefront state for `slots` paths out of one allocation.
 int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
-  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 16 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4;
+  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4;
   size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
   if (ctx->wf.bytes < bytes) {
     int rc = ensure(&ctx->wf, bytes);
@@ -1579,7 +1965,7 @@ int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
   W->hit = (dev::WfHit*)take(sizeof(dev::WfHit) * (size_t)slots);
   W->rng = (uint64_t*)take(8ull * slots);
   W->path = (uint4*)take(16ull * slots);
-  W->p0 = (float4*)take(16ull * slots);
+  W->p0 = (float4*)take(32ull * slots);  // wavefront: 1 float4/slot; lean megakernel: 2
   W->lp0 = (float2*)take(8ull * slots);
   W->lvl = (float2*)take(8ull * kMaxDepth * slots);
   W->acc = (float4*)take(16ull * slots);
@@ -1640,6 +2026,19 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   if ((uint64_t)p->sample_base + p->spp > (1ull << 20))
     return fail(FS_ERR_INVALID, "sample index must stay below 2^20 (seed layout)");
   return FS_OK;
+}
+
+enum class KernelMode { kLean, kLeanIfIf, kRegen, kLockstep, kWavefront };
+
+KernelMode kernel_mode() {
+  const char* e = std::getenv("FS_KERNEL");
+  if (!e || !*e) return KernelMode::kLean;
+  std::string m(e);
+  if (m == "regen") return KernelMode::kRegen;
+  if (m == "lean_ifif") return KernelMode::kLeanIfIf;
+  if (m == "lockstep") return KernelMode::kLockstep;
+  if (m == "wavefront") return KernelMode::kWavefront;
+  return KernelMode::kLean;
 }
 
 }  // namespace
@@ -1846,10 +2245,15 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // Long renders are split into launches of at most `chunk` samples per
   // pixel; the running mean lives in the frame, so the result is identical.
   const uint32_t chunk = 32;
-  // FS_KERNEL=1 selects the sample-lockstep kernel (A/B); default: path regeneration.
-  const int variant = std::getenv("FS_KERNEL") ? std::atoi(std::getenv("FS_KERNEL")) : 4;
+  // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
+  // produces identical frames): "lean" (default) path-regeneration megakernel
+  // with the unwind scratch in HBM rows and while-while traversal;
+  // "lean_ifif" the same with the single-loop traversal; "regen" with the unwind
+  // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
+  // extend/shade kernels over a compacted path queue.
+  const KernelMode mode = kernel_mode();
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-  if (variant == 5 && blocks && params->spp) {
+  if (mode == KernelMode::kWavefront && blocks && params->spp) {
     // Wavefront: begin -> (extend, shade)* until no path is alive.
     dev::WfState W;
     uint32_t slots = (uint32_t)(blocks * kBlock);
@@ -1901,15 +2305,26 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     return FS_OK;
   }
+  dev::WfState lean{};
+  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanIfIf;
+  if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
+    if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean))) return rc;
+  }
   for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
-    auto kern = count ? dev::render_kernel_regen<true, 2> : dev::render_kernel_regen<false, 2>;
-    if (variant == 1) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
-    if (variant == 3) kern = count ? dev::render_kernel_regen<true, 3> : dev::render_kernel_regen<false, 3>;
-    if (variant == 4) kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
-                       (DevCounters*)ctx->counters.p);
+    auto kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
+    if (mode == KernelMode::kLockstep) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
+    if (lean_mode) {
+      auto lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
+      if (mode == KernelMode::kLeanIfIf)
+        lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
+      hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
+                         lean.p0, (DevCounters*)ctx->counters.p);
+    } else {
+      hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
+                         (DevCounters*)ctx->counters.p);
+    }
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -1946,6 +2361,13 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->node_visits = c.node_visits;
   out->tri_tests = c.tri_tests;
   out->prim_tests = c.prim_tests;
+#ifdef FS_PHASE_PROF
+  std::fprintf(stderr,
+               "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "
+               "shade %llu unwind %llu - iters %llu total %llu\n",
+               c.phase[0], c.phase[1], c.phase[2], c.phase[5], c.phase[6], c.phase[7], c.phase[3], c.phase[4],
+               c.phase[8], c.phase[9]);
+#endif
   return FS_OK;
 }
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace fs {
@@ -153,7 +154,11 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
 }
 
 constexpr int kBins = 16;
-constexpr uint32_t kLeafTarget = 4;
+// Target leaf size (FS_BVH_LEAF overrides, for tuning).
+uint32_t leaf_target_env() {
+  uint32_t v = std::getenv("FS_BVH_LEAF") ? (uint32_t)std::atoi(std::getenv("FS_BVH_LEAF")) : 2u;
+  return (v && v <= kMaxLeafCount) ? v : 2u;
+}
 
 class BvhBuilder {
  public:
@@ -166,7 +171,7 @@ class BvhBuilder {
     prims_ = &prims;
     uint32_t root = alloc_node();
     Box all = range_box(0, (uint32_t)prims.size());
-    if (prims.size() <= kLeafTarget) {
+    if (prims.size() <= leaf_) {
       set_child(root, 0, all, make_leaf(0, (uint32_t)prims.size()));
       set_child(root, 1, Box(), kLeafBit);  // empty
     } else {
@@ -243,7 +248,7 @@ class BvhBuilder {
       if (cmax[k] - cmin[k] > cmax[axis] - cmin[axis]) axis = k;
     // Depth guard: fall back to an object median near the stack bound.
     uint32_t need = 0;
-    for (uint32_t m = n; m > kLeafTarget; m = (m + 1) / 2) need++;
+    for (uint32_t m = n; m > leaf_; m = (m + 1) / 2) need++;
     bool median = depth + need + 1 >= kTraversalStack - 1 || cmax[axis] <= cmin[axis];
     if (!median) {
       float best_cost = INFINITY;
@@ -307,7 +312,7 @@ class BvhBuilder {
     for (int s = 0; s < 2; s++) {
       uint32_t cb = ranges[s][0], ce = ranges[s][1];
       Box cbox = range_box(cb, ce);
-      if (ce - cb <= kLeafTarget || depth + 1 >= kTraversalStack - 1) {
+      if (ce - cb <= leaf_ || depth + 1 >= kTraversalStack - 1) {
         set_child(node, s, cbox, make_leaf(cb, ce));
       } else {
         uint32_t c = alloc_node();
@@ -323,6 +328,7 @@ class BvhBuilder {
   const std::vector<DevTri>* mesh_tris_;
   const std::vector<float>* mesh_normals_;
   std::vector<Prim>* prims_ = nullptr;
+  uint32_t leaf_ = leaf_target_env();
   uint32_t max_depth_ = 0;
   bool overflow_ = false;
 };
@@ -395,6 +401,18 @@ int build_object(const fs_object& o, DevObject* out, std::string* err) {
         for (int i = 0; i < 8; i++) v[i] = rotate(v[i] - center, c, s, axis) + center;
       }
       cube_planes(v, out->d);
+      {  // padded corner box, same padding rule as the BVH node boxes
+        f3 mn = v[0], mx = v[0];
+        for (int i = 1; i < 8; i++) {
+          mn = mk3(std::min(mn.x, v[i].x), std::min(mn.y, v[i].y), std::min(mn.z, v[i].z));
+          mx = mk3(std::max(mx.x, v[i].x), std::max(mx.y, v[i].y), std::max(mx.z, v[i].z));
+        }
+        float sc = 1.0f;
+        for (float c : {mn.x, mn.y, mn.z, mx.x, mx.y, mx.z}) sc = std::max(sc, std::fabs(c));
+        float pd = 1e-4f * sc;
+        put3(out->d + 24, mn - mk3(pd, pd, pd));
+        put3(out->d + 27, mx + mk3(pd, pd, pd));
+      }
       return FS_OK;
     }
     case FS_OBJ_QUAD_ONWH: {  // object.cpp:167-189

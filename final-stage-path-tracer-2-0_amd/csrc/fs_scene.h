@@ -12,7 +12,7 @@
 
 namespace fs {
 
-// Object record, 128 B; read wave-uniformly by the object loop of
+// Object record, 192 B; read wave-uniformly by the object loop of
 // Scene::Trace (scene.cpp:231-233), so it is fetched with scalar loads.
 struct DevObject {
   int32_t kind;  // fs_object_kind (QUAD_PUV is stored as QUAD_ONWH)
@@ -21,16 +21,17 @@ struct DevObject {
   int32_t i1;    // MESH: 1 if the mesh has vertex normals
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
   int32_t i3, i4, i5;
-  float d[24];
+  float d[40];
   // SPHERE  d0-2 center, d3 radius
   // PLANE   d0-3 plane
   // DISC    d0-3 plane, d4-6 origin, d7 radius
-  // CUBOID  d0-23 six face planes (volume.cpp:234-247)
+  // CUBOID  d0-23 six face planes (volume.cpp:234-247); d24-29 padded box
+  //         of the 8 corners (a conservative cull, not a reference test)
   // QUAD    d0-3 plane, d4-6 origin, d7 half width, d8 half height,
   //         d9-11 bitangent, d12-14 tangent
   // MESH    d0-5 reference root bounds (min, max) — mesh.cpp:129-133
 };
-static_assert(sizeof(DevObject) == 128, "DevObject layout");
+static_assert(sizeof(DevObject) == 192, "DevObject layout");
 
 // BVH2 node, 64 B: both child boxes (SoA over the two children) + child words.
 // Child word: bit31 set -> leaf, bits 24..30 = triangle count, bits 0..23 =

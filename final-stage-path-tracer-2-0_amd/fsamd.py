@@ -147,7 +147,8 @@ def gpu_lib():
     """libfsgpu.so (HIP kernels + C ABI). Raises if it has not been built."""
     global _gpu
     if _gpu is None:
-        path = os.path.join(PKG_DIR, "libfsgpu.so")
+        # FSAMD_GPU_LIB selects a measurement build (libfsgpu_prof.so).
+        path = os.environ.get("FSAMD_GPU_LIB") or os.path.join(PKG_DIR, "libfsgpu.so")
         if not os.path.exists(path):
             raise FsError(f"{path} missing: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
         _gpu = _bind(C.CDLL(path, mode=C.RTLD_GLOBAL), GPU_SYMBOLS)

@@ -1,5 +1,6 @@
 """Interleaved A/B of kernel variants (FS_KERNEL env) in one process.
-usage: python tools/perf_ab.py variants scenes [spp] [rounds]"""
+usage: python tools/perf_ab.py modes scenes [spp] [rounds]
+(modes: lean, regen, lockstep, wavefront — see kernel_mode() in fs_device.hip)"""
 import os
 import sys
 import time

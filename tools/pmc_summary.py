@@ -1,0 +1,59 @@
+"""Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh for one kernel.
+
+usage: python tools/pmc_summary.py gpurun_out/<round>/pmc KERNEL_SUBSTR OUT.json [note]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 128-B read requests at
+64 B, so it is doubled; WRITE_SIZE is taken as is. Infinity-Cache hits are
+counted by both, so this is L2-miss (fabric) traffic, an upper bound on HBM.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    pmc_dir, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    note = sys.argv[4] if len(sys.argv) > 4 else ""
+    vals = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "*", "*counter_collection.csv"))):
+        for row in csv.DictReader(open(f)):
+            if kname not in row["Kernel_Name"]:
+                continue
+            key = (f, row["Dispatch_Id"])
+            vals[row["Counter_Name"]][key] += float(row["Counter_Value"])
+            meta = {"kernel": row["Kernel_Name"].split("(")[0], "vgpr": int(row["VGPR_Count"]),
+                    "agpr": int(row["Accum_VGPR_Count"]), "sgpr": int(row["SGPR_Count"]),
+                    "scratch_bytes_per_lane": int(row["Scratch_Size"]), "grid": int(row["Grid_Size"])}
+    if not vals:
+        raise SystemExit(f"no dispatches of {kname!r} under {pmc_dir}")
+    avg = {c: sum(d.values()) / len(d) for c, d in vals.items()}
+    res = dict(meta)
+    res["dispatches"] = {c: len(d) for c, d in vals.items()}
+    res["counters_avg_per_dispatch"] = {c: round(v, 3) for c, v in sorted(avg.items())}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        fetch = avg["FETCH_SIZE"] * 1024 * 2
+        write = avg["WRITE_SIZE"] * 1024
+        res["fetch_bytes_per_launch"] = fetch
+        res["write_bytes_per_launch"] = write
+        res["hbm_bytes_per_launch"] = round(fetch + write)
+    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+        res["l2_hit_rate"] = round(avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1), 4)
+    if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
+        res["wait_any_frac"] = round(avg["SQ_WAIT_ANY"] / max(avg["SQ_WAVE_CYCLES"], 1), 4)
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        res["valu_lane_util"] = round(avg["SQ_THREAD_CYCLES_VALU"] / max(64 * avg["SQ_ACTIVE_INST_VALU"], 1), 4)
+    res["method"] = ("rocprofv3 --pmc, one counter group per pass (tools/gpu_pmc.sh); FETCH_SIZE KiB x1024 x2 "
+                     "(gfx950 half-count, MI355X_MICROARCH.md §HBM) + WRITE_SIZE KiB x1024; per dispatch average")
+    if note:
+        res["note"] = note
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
