@@ -953,6 +953,7 @@ struct WfState {
   uint64_t* aov_id;
   uint32_t* list0;
   uint32_t* list1;
+  uint32_t* ovf;    // lean megakernel: BVH4 stack overflow rows
   uint32_t* count;  // [0], [1]: active counts
 };
 
@@ -1169,6 +1170,106 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
 }
 
 // Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
+// Per-lane traversal stack: kTraversalStack entries in LDS (column per lane),
+// deeper entries in a per-lane HBM row (BVH4 only; rarely touched).
+struct LaneStack {
+  uint32_t* lds;  // stk_all + lane, stride kBlock
+  uint32_t* ovf;  // wave row base + lane, stride kBlock
+  __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
+    if (sp < kTraversalStack)
+      lds[sp * kBlock] = v;
+    else
+      ovf[(sp - kTraversalStack) * kBlock] = v;
+    sp++;
+  }
+  __device__ __forceinline__ uint32_t pop(uint32_t& sp, uint32_t none) const {
+    if (sp == 0) return none;
+    --sp;
+    return sp < kTraversalStack ? lds[sp * kBlock] : ovf[(sp - kTraversalStack) * kBlock];
+  }
+};
+
+// BVH4 closest-hit traversal, while-while with postponed leaves as
+// traverse_ww. The hit children are ordered near to far by a 4-input sorting
+// network; the nearest is taken next and the rest pushed far-first.
+template <bool COUNT>
+__device__ __forceinline__ void traverse4_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
+                                             MinHit& h, const LaneStack& st, Tally<COUNT>& tally) {
+  constexpr uint32_t kNone = 0x7FFFFFFFu;
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
+  uint32_t w = root, leaf = 0, sp = 0;
+  while (w != kNone || leaf) {
+    while (!(w & kLeafBit) && w != kNone) {
+      const float4* q = reinterpret_cast<const float4*>(S.nodes4 + w);
+      float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
+      uint4 Cw = reinterpret_cast<const uint4*>(q)[6];
+      if (COUNT) tally.nodes += 2;  // counted in 64-B units
+      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+      float k0, k1, k2, k3;  // entry distance, +inf when the child is missed
+      if (!zl) {
+        auto slab = [&](float lx, float hx, float ly, float hy, float lz, float hz) {
+          float a = fmaf(lx, ix, ox), b = fmaf(hx, ix, ox);
+          float c = fmaf(ly, iy, oy), d = fmaf(hy, iy, oy);
+          float e = fmaf(lz, iz, oz), f = fmaf(hz, iz, oz);
+          float tn = fmaxf(fmaxf(fminf(a, b), fminf(c, d)), fmaxf(fminf(e, f), -1e-6f));
+          float tf = fminf(fminf(fmaxf(a, b), fmaxf(c, d)), fminf(fmaxf(e, f), tmax_lim));
+          return tn <= tf ? tn : kInfinity;
+        };
+        k0 = slab(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x);
+        k1 = slab(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y);
+        k2 = slab(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z);
+        k3 = slab(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w);
+      } else {
+        f3 s = r.start;
+        auto inside = [&](float lx, float hx, float ly, float hy, float lz, float hz) {
+          return s.x >= lx && s.x <= hx && s.y >= ly && s.y <= hy && s.z >= lz && s.z <= hz ? 0.0f : kInfinity;
+        };
+        k0 = inside(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x);
+        k1 = inside(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y);
+        k2 = inside(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z);
+        k3 = inside(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w);
+      }
+      uint32_t c0 = Cw.x, c1 = Cw.y, c2 = Cw.z, c3 = Cw.w;
+      auto cx = [](float& ka, uint32_t& ca, float& kb, uint32_t& cb) {
+        bool sw = kb < ka;
+        float tk = sw ? kb : ka;
+        kb = sw ? ka : kb;
+        ka = tk;
+        uint32_t tc = sw ? cb : ca;
+        cb = sw ? ca : cb;
+        ca = tc;
+      };
+      cx(k0, c0, k1, c1);
+      cx(k2, c2, k3, c3);
+      cx(k0, c0, k2, c2);
+      cx(k1, c1, k3, c3);
+      cx(k1, c1, k2, c2);
+      if (k3 < kInfinity) st.push(sp, c3);
+      if (k2 < kInfinity) st.push(sp, c2);
+      if (k1 < kInfinity) st.push(sp, c1);
+      w = k0 < kInfinity ? c0 : st.pop(sp, kNone);
+      if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
+        leaf = w;
+        w = st.pop(sp, kNone);
+      }
+      if (__ballot(leaf == 0) == 0) break;
+    }
+    while (leaf) {
+      test_leaf<COUNT>(S, leaf, oi, r, zl, h, tally);
+      leaf = 0;
+      if (w & kLeafBit) {
+        leaf = w;
+        w = st.pop(sp, kNone);
+      }
+    }
+  }
+}
+
 // Conservative segment-vs-box cull for analytic objects (not a reference
 // test): the slab interval uses v_rcp and the same t margins as the BVH
 // traversal, against a box padded on the host (fs_scene.cpp). A segment that
@@ -1197,10 +1298,10 @@ struct PhaseAcc {};
 #define FS_TICK() 0ull
 #endif
 
-template <bool COUNT, bool WW = false>
+template <bool COUNT, bool WW = false, bool WIDE = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
-                                                PhaseAcc& pa) {
+                                                PhaseAcc& pa, uint32_t* __restrict__ ovf = nullptr) {
   h.t = 2.0f;
   h.obj = -1;
   h.prim = 0;
@@ -1217,7 +1318,9 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       bool visit = ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
       uint64_t t1 = FS_TICK();
       if (visit) {
-        if (WW)
+        if (WIDE && o->i3 >= 0)
+          traverse4_ww<COUNT>(S, (uint32_t)o->i3, (int32_t)oi, r, zl, h, LaneStack{stk, ovf}, tally);
+        else if (WW)
           traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
         else
           traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
@@ -1573,10 +1676,11 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool WW = false>
+template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
+                                                                     uint32_t* __restrict__ ovf_all,
                                                                      DevCounters* __restrict__ counters) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
   const uint32_t lane = threadIdx.x;
@@ -1586,6 +1690,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   float2* lvl = lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
   float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
+  uint32_t* ovf = ovf_all + (size_t)blockIdx.x * (kStackOverflow * kBlock) + lane;
 
   uint32_t x, y;
   {
@@ -1649,13 +1754,13 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       MinHit h;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW>(S, r, h, stk, tally, pa);
+      scene_trace_min<COUNT, WW, WIDE>(S, r, h, stk, tally, pa, ovf);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW>(S, r, h, stk, tally, pa);
+      scene_trace_min<COUNT, WW, WIDE>(S, r, h, stk, tally, pa, ovf);
 #endif
       FS_PHASE(2);
       if (h.obj < 0) {
@@ -1863,7 +1968,7 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, tris, tri_normals, materials, table, counters, pack_send, pack_recv;
+  DevBuf objects, nodes, nodes4, tris, tri_normals, materials, table, counters, pack_send, pack_recv;
   DevScene scene{};
   uint32_t num_objects = 0;
   PreparedScene host;
@@ -1945,7 +2050,8 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 
 // Carves the wavefront state for `slots` paths out of one allocation.
 int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
-  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4;
+  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4 +
+               4 * kStackOverflow;
   size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
   if (ctx->wf.bytes < bytes) {
     int rc = ensure(&ctx->wf, bytes);
@@ -1974,6 +2080,7 @@ int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
   W->aov_id = (uint64_t*)take(8ull * slots);
   W->list0 = (uint32_t*)take(4ull * slots);
   W->list1 = (uint32_t*)take(4ull * slots);
+  W->ovf = (uint32_t*)take(4ull * kStackOverflow * slots);
   if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "wavefront state overflow");
   if (!ctx->host_count) FS_HIP(hipHostMalloc((void**)&ctx->host_count, 16, hipHostMallocDefault));
   return FS_OK;
@@ -2028,7 +2135,7 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   return FS_OK;
 }
 
-enum class KernelMode { kLean, kLeanIfIf, kRegen, kLockstep, kWavefront };
+enum class KernelMode { kLean, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
 
 KernelMode kernel_mode() {
   const char* e = std::getenv("FS_KERNEL");
@@ -2036,6 +2143,7 @@ KernelMode kernel_mode() {
   std::string m(e);
   if (m == "regen") return KernelMode::kRegen;
   if (m == "lean_ifif") return KernelMode::kLeanIfIf;
+  if (m == "lean_bvh4") return KernelMode::kLeanBvh4;
   if (m == "lockstep") return KernelMode::kLockstep;
   if (m == "wavefront") return KernelMode::kWavefront;
   return KernelMode::kLean;
@@ -2080,7 +2188,7 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->materials, &ctx->table,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->materials, &ctx->table,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
     b->release();
   ctx->wf.release();
@@ -2104,6 +2212,7 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   ctx->have_scene = false;
   if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
   if ((rc = upload(ctx, &ctx->nodes, P.nodes.data(), P.nodes.size() * sizeof(BvhNode)))) return rc;
+  if ((rc = upload(ctx, &ctx->nodes4, P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node)))) return rc;
   if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri)))) return rc;
   if ((rc = upload(ctx, &ctx->tri_normals, P.tri_normals.data(), P.tri_normals.size() * sizeof(float)))) return rc;
   if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
@@ -2113,6 +2222,7 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   DevScene& S = ctx->scene;
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
+  S.nodes4 = (const Bvh4Node*)ctx->nodes4.p;
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
@@ -2146,7 +2256,7 @@ int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms, uint64_
   if (num_triangles) *num_triangles = ctx->host.tris.size();
   if (num_nodes) *num_nodes = ctx->host.nodes.size();
   if (device_bytes)
-    *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
+    *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->nodes4.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
                      ctx->materials.bytes + ctx->table.bytes;
   return FS_OK;
 }
@@ -2248,7 +2358,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
   // produces identical frames): "lean" (default) path-regeneration megakernel
   // with the unwind scratch in HBM rows and while-while traversal;
-  // "lean_ifif" the same with the single-loop traversal; "regen" with the unwind
+  // "lean_bvh4" with 4-wide nodes for scenes uploaded with FS_BVH4=1 (slower:
+  // more VALU per step); "lean_ifif" the single-loop traversal; "regen" with the unwind
   // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
   // extend/shade kernels over a compacted path queue.
   const KernelMode mode = kernel_mode();
@@ -2306,7 +2417,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     return FS_OK;
   }
   dev::WfState lean{};
-  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanIfIf;
+  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanBvh4 || mode == KernelMode::kLeanIfIf;
   if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
     if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean))) return rc;
   }
@@ -2317,10 +2428,12 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     if (mode == KernelMode::kLockstep) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
     if (lean_mode) {
       auto lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
+      if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
+        lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
       if (mode == KernelMode::kLeanIfIf)
         lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
       hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
-                         lean.p0, (DevCounters*)ctx->counters.p);
+                         lean.p0, lean.ovf, (DevCounters*)ctx->counters.p);
     } else {
       hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
                          (DevCounters*)ctx->counters.p);

@@ -18,6 +18,7 @@ constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS col
 struct DevScene {
   const DevObject* __restrict__ objects;
   const BvhNode* __restrict__ nodes;
+  const Bvh4Node* __restrict__ nodes4;
   const DevTri* __restrict__ tris;
   const float4* __restrict__ tri_normals;
   const fs_material* __restrict__ materials;

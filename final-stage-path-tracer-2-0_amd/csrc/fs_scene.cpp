@@ -333,6 +333,98 @@ class BvhBuilder {
   bool overflow_ = false;
 };
 
+// Collapses a BVH2 into a BVH4: a node's four slots are filled by repeatedly
+// opening the inner child with the largest box surface. Leaves and their
+// triangle ranges are shared with the BVH2. Returns the BVH4 root, or -1 when
+// the worst-case traversal stack (sum over a root-to-leaf path of the pushes
+// per node) would not fit kTraversalStack + kStackOverflow.
+class Collapse4 {
+ public:
+  Collapse4(const std::vector<BvhNode>& n2, std::vector<Bvh4Node>* n4) : n2_(n2), n4_(n4) {}
+  int32_t run(uint32_t root2) {
+    size_t mark = n4_->size();
+    uint32_t need = 0;
+    uint32_t r = node(root2, &need);
+    if (need + 1 > kTraversalStack + kStackOverflow) {
+      n4_->resize(mark);
+      return -1;
+    }
+    return (int32_t)r;
+  }
+
+ private:
+  struct Slot {
+    float lo[3], hi[3];
+    uint32_t word;
+    float area() const {
+      float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+      return dx * dy + dy * dz + dz * dx;
+    }
+  };
+  static bool empty_slot(const BvhNode& n, int s) { return (n.child[s] & kLeafBit) && n.lo_x[s] >= 1e30f; }
+  static Slot slot_of(const BvhNode& n, int s) {
+    Slot o;
+    o.lo[0] = n.lo_x[s];
+    o.lo[1] = n.lo_y[s];
+    o.lo[2] = n.lo_z[s];
+    o.hi[0] = n.hi_x[s];
+    o.hi[1] = n.hi_y[s];
+    o.hi[2] = n.hi_z[s];
+    o.word = n.child[s];
+    return o;
+  }
+  uint32_t node(uint32_t i2, uint32_t* need) {
+    std::vector<Slot> slots;
+    for (int s = 0; s < 2; s++)
+      if (!empty_slot(n2_[i2], s)) slots.push_back(slot_of(n2_[i2], s));
+    while (slots.size() < 4) {
+      int best = -1;
+      for (size_t k = 0; k < slots.size(); k++)
+        if (!(slots[k].word & kLeafBit) && (best < 0 || slots[k].area() > slots[best].area())) best = (int)k;
+      if (best < 0) break;
+      const BvhNode& c = n2_[slots[best].word];
+      slots.erase(slots.begin() + best);
+      for (int s = 0; s < 2; s++)
+        if (!empty_slot(c, s)) slots.push_back(slot_of(c, s));
+    }
+    uint32_t me = (uint32_t)n4_->size();
+    n4_->emplace_back();
+    uint32_t sub = 0;
+    for (size_t k = 0; k < slots.size(); k++) {
+      if (!(slots[k].word & kLeafBit)) {
+        uint32_t cn = 0;
+        slots[k].word = node(slots[k].word, &cn);
+        sub = std::max(sub, cn);
+      }
+    }
+    Bvh4Node& o = (*n4_)[me];
+    std::memset(&o, 0, sizeof(o));
+    for (int k = 0; k < 4; k++) {
+      if (k < (int)slots.size()) {
+        const Slot& sl = slots[k];
+        o.lo_x[k] = sl.lo[0], o.lo_y[k] = sl.lo[1], o.lo_z[k] = sl.lo[2];
+        o.hi_x[k] = sl.hi[0], o.hi_y[k] = sl.hi[1], o.hi_z[k] = sl.hi[2];
+        o.child[k] = sl.word;
+      } else {
+        o.lo_x[k] = o.lo_y[k] = o.lo_z[k] = o.hi_x[k] = o.hi_y[k] = o.hi_z[k] = 3e30f;
+        o.child[k] = kLeafBit;  // empty leaf
+      }
+    }
+    uint32_t pushes = slots.empty() ? 0 : (uint32_t)slots.size() - 1;
+    *need = pushes + sub;
+    return me;
+  }
+  const std::vector<BvhNode>& n2_;
+  std::vector<Bvh4Node>* n4_;
+};
+
+// BVH4 collapse is opt-in (FS_BVH4=1, FS_KERNEL=lean_bvh4): measured slower
+// than the BVH2 on MI355X.
+bool bvh4_enabled() {
+  const char* e = std::getenv("FS_BVH4");
+  return e && std::atoi(e) != 0;
+}
+
 void cube_planes(const f3* v, float* d) {  // volume.cpp:234-247
   f4 p[6] = {plane_3p(v[0], v[1], v[2]), plane_3p(v[6], v[5], v[4]), plane_3p(v[5], v[6], v[2]),
              plane_3p(v[7], v[4], v[0]), plane_3p(v[4], v[5], v[1]), plane_3p(v[6], v[7], v[3])};
@@ -491,11 +583,13 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
   // Meshes: MeshObject::MeshObject + BuildBvh face planes.
   struct MeshOut {
     uint32_t root = 0;
+    int32_t root4 = -1;
     bool tree = false;
     bool normals = false;
     Bounds rb;
   };
   std::vector<MeshOut> mesh_out(d->num_meshes);
+  const bool use4 = bvh4_enabled();
   bool any_normals = false;
   for (uint32_t mi = 0; mi < d->num_meshes; mi++)
     if (d->meshes[mi].normals && d->meshes[mi].num_normals) any_normals = true;
@@ -601,6 +695,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
       return FS_ERR_INVALID;
     }
+    mesh_out[mi].root4 = use4 ? Collapse4(S.nodes, &S.nodes4).run(mesh_out[mi].root) : -1;
   }
 
   S.objects.resize(d->num_objects);
@@ -623,6 +718,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       D.i0 = (int32_t)mo.root;
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
+      D.i3 = mo.tree ? mo.root4 : -1;
       put3(D.d, mo.rb.mn);
       put3(D.d + 3, mo.rb.mx);
     } else {

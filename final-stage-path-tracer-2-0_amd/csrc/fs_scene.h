@@ -20,7 +20,8 @@ struct DevObject {
   int32_t i0;    // MESH: BVH root node index
   int32_t i1;    // MESH: 1 if the mesh has vertex normals
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
-  int32_t i3, i4, i5;
+  int32_t i3;    // MESH: BVH4 root node index, or -1 (traverse the BVH2)
+  int32_t i4, i5;
   float d[40];
   // SPHERE  d0-2 center, d3 radius
   // PLANE   d0-3 plane
@@ -44,10 +45,25 @@ struct BvhNode {
   uint32_t pad[2];
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+// BVH4 node, 128 B: four child boxes (SoA over the children) + 4 child
+// words, collapsed from the BVH2 (fs_scene.cpp collapse4). Same child-word
+// encoding; an unused slot is an empty leaf (count 0) with a far point box.
+struct Bvh4Node {
+  float lo_x[4], hi_x[4];
+  float lo_y[4], hi_y[4];
+  float lo_z[4], hi_z[4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kMaxLeafCount = 127;
 constexpr uint32_t kMaxTriangles = 1u << 24;
 constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
+// BVH4 traversal keeps kTraversalStack entries in LDS and spills deeper ones
+// to a per-lane HBM row of kStackOverflow entries; a mesh whose worst-case
+// stack need exceeds the sum keeps the BVH2 (collapse4 checks).
+constexpr uint32_t kStackOverflow = 40;
 
 // Triangle record, 80 B: the operands of the reference test
 // (intersect.cpp:357-419) with every ray-independent term precomputed on the
@@ -73,6 +89,7 @@ static_assert(sizeof(DevTri) == 80, "DevTri layout");
 struct PreparedScene {
   std::vector<DevObject> objects;
   std::vector<BvhNode> nodes;
+  std::vector<Bvh4Node> nodes4;
   std::vector<DevTri> tris;
   std::vector<float> tri_normals;  // 12 floats per triangle (n0,n1,n2 + pad) or empty
   std::vector<fs_material> materials;
