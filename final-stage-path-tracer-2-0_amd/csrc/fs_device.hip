@@ -586,23 +586,32 @@ __device__ __forceinline__ T* at_byte(T* base, uint32_t off) {
   return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
 }
 
+// texrow: per-level SampleDiffuse result of a textured material (lean kernel
+// only; other schedules pass nullptr and never see a textured scene).
+template <bool TEX = false>
 __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t mats_lo, uint32_t mats_hi,
                                      const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
-                                     int stride = kBlock, uint32_t lane = 0) {
+                                     int stride = kBlock, uint32_t lane = 0,
+                                     const float4* __restrict__ texrow = nullptr) {
   for (int k = top; k >= 0; --k) {
     const fs_material& m = S.materials[mat_of(mats_lo, mats_hi, k)];
     float2 cs = *at_byte(lvl, ((uint32_t)k * (uint32_t)stride + lane) * 8u);
     f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
+    f3 sd = dif;  // SampleDiffuse (material.cpp:108-126)
+    if (TEX && m.texture >= 0) {
+      float4 tx = *at_byte(texrow, ((uint32_t)k * (uint32_t)stride + lane) * 16u);
+      sd = mk3(tx.x, tx.y, tx.z);
+    }
     switch (m.kind) {
-      case FS_MAT_LIGHT:
-        L = mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
+      case FS_MAT_LIGHT:  // material.cpp:43-53
+        L = (TEX && m.texture >= 0) ? sd : mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
         break;
       case FS_MAT_DIFFUSE:
-        L = (dif * L) * cs.x;
+        L = (sd * L) * cs.x;
         break;
       case FS_MAT_METAL: {
-        f3 dc = (dif * L) * cs.x;
-        f3 rc = dif * L;
+        f3 dc = (sd * L) * cs.x;
+        f3 rc = sd * L;
         L = dc * m.roughness + rc * (float)(1.0 - (double)m.roughness);
         break;
       }
@@ -613,7 +622,7 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t 
         break;
       case FS_MAT_CERAMIC:
       case FS_MAT_GLOW: {
-        f3 dc = (dif * L) * cs.x;
+        f3 dc = (sd * L) * cs.x;
         L = L * cs.y + dc * (float)(1.0 - (double)cs.y);
         if (m.kind == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
         break;
@@ -954,6 +963,7 @@ struct WfState {
   uint32_t* list0;
   uint32_t* list1;
   uint32_t* ovf;    // lean megakernel: BVH4 stack overflow rows
+  float4* tex;      // lean megakernel: per-level texel rows (textured scenes)
   uint32_t* count;  // [0], [1]: active counts
 };
 
@@ -975,6 +985,7 @@ struct MinHit {
   float t, u, v;
   int32_t obj;
   uint32_t prim, point;
+  int32_t tc;  // last object that wrote surface_texcoords (-1: still vector2())
 };
 
 // BVH2 traversal of one mesh, closest-hit bookkeeping only (no point/normal).
@@ -1298,7 +1309,7 @@ struct PhaseAcc {};
 #define FS_TICK() 0ull
 #endif
 
-template <bool COUNT, bool WW = false, bool WIDE = false>
+template <bool COUNT, bool WW = false, bool WIDE = false, bool TEX = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, uint32_t* __restrict__ ovf = nullptr) {
@@ -1307,6 +1318,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   h.prim = 0;
   h.u = h.v = 0.0f;
   h.point = 0;
+  h.tc = -1;
   bool zl = zero_len(r);
   for (uint32_t oi = 0; oi < S.num_objects; ++oi) {
     const DevObject* __restrict__ o = S.objects + oi;
@@ -1325,6 +1337,9 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         else
           traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
       }
+      // MeshObject::Trace writes surface_texcoords only when the mesh has
+      // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
+      if (TEX && h.obj == (int32_t)oi && o->i4) h.tc = (int32_t)oi;
 #ifdef FS_PHASE_PROF
       uint64_t t2 = FS_TICK();
       pa.cull += t1 - t0;
@@ -1388,6 +1403,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         }
       }
     }
+    if (TEX && h.obj == (int32_t)oi) h.tc = (int32_t)oi;  // analytic objects always write texcoords
 #ifdef FS_PHASE_PROF
     pa.prim += FS_TICK() - tp0;
 #endif
@@ -1641,11 +1657,112 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene S, DevCamera C, DevF
 }
 
 
+// ---- textures (material.cpp:108-126, intersect.cpp:769-784) -------------
+// planar_map_texcoords
+__device__ __forceinline__ void planar_tc(f3 p, f3 n, float& u, float& v) {
+  if (n.x > n.y && n.x > n.z) {
+    u = p.y;
+    v = p.z;
+  } else if (n.y > n.x && n.y > n.z) {
+    u = p.x;
+    v = p.z;
+  } else {
+    u = p.x;
+    v = p.y;
+  }
+}
+// sphere_map_texcoords: float atan2 overload, float BASE_PI, double +0.5/*0.5/1.0-.
+// atan2f is ocml's here and the C runtime's in the reference (tolerance).
+__device__ __forceinline__ void sphere_tc(f3 n, float& u, float& v) {
+  float uu = (float)((double)(atan2f(n.x, n.z) / (2 * kPi)) + 0.5);
+  float vv = (float)((double)n.y * 0.5 + 0.5);
+  u = uu;
+  v = (float)(1.0 - (double)vv);
+}
+// float -> uint32 as x86-64 compilers lower it: truncate to int64, keep the
+// low half; NaN and |f| >= 2^63 give 0.
+__device__ __forceinline__ uint32_t f2u32_x64(float f) {
+  if (!(f > -9.2233715e18f && f < 9.2233715e18f)) return 0u;
+  return (uint32_t)(uint64_t)(int64_t)f;
+}
+// DiffuseMaterial::SampleDiffuse for a material with a map (texture >= 0).
+__device__ __forceinline__ f3 sample_tex(const DevScene& S, const fs_material& m, float tu, float tv) {
+  uint4 ti = S.tex_info[m.texture];
+  float fx = (tu * m.texture_scale * (float)ti.y + 0.5f) - 1;
+  float fy = (tv * m.texture_scale * (float)ti.z + 0.5f) - 1;
+  uint32_t x = f2u32_x64(fx) % ti.y, y = f2u32_x64(fy) % ti.z;
+  uint32_t off = y * ti.y * 3 + x * 3;
+  const float* t = S.tex_rgb + ti.x + off;
+  return mk3(t[0], t[1], t[2]);
+}
+
+// Texcoords written by object `oi`'s own hit on ray r (when a later mesh
+// without texcoords took the hit, the reference keeps these; rare, so the
+// object is intersected again here instead of carrying them through the
+// traversal).
+template <bool COUNT>
+__device__ __forceinline__ void stale_texcoords(const DevScene& S, const Ray& r, int32_t oi, uint32_t* __restrict__ stk,
+                                             float& tu, float& tv) {
+  const DevObject* __restrict__ o = S.objects + oi;
+  const float* d = o->d;
+  float t;
+  f3 p, n;
+  tu = tv = 0.0f;
+  switch (o->kind) {
+    case FS_OBJ_SPHERE:
+      if (ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n)) sphere_tc(n, tu, tv);
+      break;
+    case FS_OBJ_PLANE:
+    case FS_OBJ_DISC:
+    case FS_OBJ_QUAD_ONWH:
+      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p)) planar_tc(p, mk3(d[0], d[1], d[2]), tu, tv);
+      break;
+    case FS_OBJ_CUBOID: {
+      float best = 2.0f;
+      for (uint32_t i = 0; i < 6; i++) {
+        if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, t, p) && t < best) {
+          bool ok = true;
+          for (uint32_t j = 0; j < 6; j++)
+            if (i / 2 != j / 2 && plane_dist(mk4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]), p) > 0.0f) ok = false;
+          if (ok) {
+            best = t;
+            planar_tc(p, mk3(d[4 * i], d[4 * i + 1], d[4 * i + 2]), tu, tv);
+            tu = tu * 0.1f;
+            tv = tv * 0.1f;
+          }
+        }
+      }
+      break;
+    }
+    default: {  // a mesh with texcoords: its own closest face
+      MinHit m;
+      m.t = 2.0f;
+      m.obj = -1;
+      m.prim = 0;
+      m.u = m.v = 0.0f;
+      m.point = 0;
+      m.tc = -1;
+      Tally<false> tally;
+      traverse_ww<false>(S, (uint32_t)o->i0, oi, r, zero_len(r), m, stk, tally);
+      if (m.obj == oi) {
+        const float2* q = S.tri_tex + 3 * (size_t)m.prim;
+        float2 t0 = q[0], t1 = q[1], t2 = q[2];
+        tu = (t0.x + (t1.x - t0.x) * m.u) + (t2.x - t0.x) * m.v;
+        tv = (t0.y + (t1.y - t0.y) * m.u) + (t2.y - t0.y) * m.v;
+      }
+      break;
+    }
+  }
+}
+
 // Rebuilds the hit point/normal of a MinHit exactly as the object tests
 // produced them (object.cpp, mesh.cpp:289-298) and applies the back-face
-// flip of Scene::Trace (scene.cpp:238-247).
+// flip of Scene::Trace (scene.cpp:238-247). For a material with a map the
+// surface texcoords follow (object.cpp:31-232, mesh.cpp:300-311), from the
+// unflipped normal.
+template <bool TEX>
 __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, const MinHit& h, f3& p, f3& n,
-                                            int32_t& mat) {
+                                            int32_t& mat, float& tu, float& tv, uint32_t* __restrict__ stk) {
   const DevObject* __restrict__ o = S.objects + h.obj;
   const float* d = o->d;
   p = h.point ? r.start : r.start + r.dir * h.t;
@@ -1667,20 +1784,40 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
   } else {
     n = mk3(d[0], d[1], d[2]);
   }
+  mat = o->mat;
+  tu = tv = 0.0f;
+  if (TEX && S.materials[mat].texture >= 0 && h.tc >= 0) {
+    if (h.tc != h.obj) {
+      stale_texcoords<false>(S, r, h.tc, stk, tu, tv);
+    } else if (kind == FS_OBJ_MESH) {
+      const float2* q = S.tri_tex + 3 * (size_t)h.prim;
+      float2 t0 = q[0], t1 = q[1], t2 = q[2];
+      tu = (t0.x + (t1.x - t0.x) * h.u) + (t2.x - t0.x) * h.v;
+      tv = (t0.y + (t1.y - t0.y) * h.u) + (t2.y - t0.y) * h.v;
+    } else if (kind == FS_OBJ_SPHERE) {
+      sphere_tc(n, tu, tv);
+    } else {
+      planar_tc(p, n, tu, tv);
+      if (kind == FS_OBJ_CUBOID) {
+        tu = tu * 0.1f;
+        tv = tv * 0.1f;
+      }
+    }
+  }
   f4 cp = plane_np(n, p);
   if (plane_dist(cp, r.start) < 0.0f) n = n * (float)-1.0;
-  mat = o->mat;
 }
 
 // Path regeneration with a lean register footprint: the closest-hit query
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false>
+template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
                                                                      uint32_t* __restrict__ ovf_all,
+                                                                     float4* __restrict__ tex_all,
                                                                      DevCounters* __restrict__ counters) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
   const uint32_t lane = threadIdx.x;
@@ -1691,6 +1828,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
   uint32_t* ovf = ovf_all + (size_t)blockIdx.x * (kStackOverflow * kBlock) + lane;
+  float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   uint32_t x, y;
   {
@@ -1754,18 +1892,23 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       MinHit h;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW, WIDE>(S, r, h, stk, tally, pa, ovf);
+      scene_trace_min<COUNT, WW, WIDE, TEX>(S, r, h, stk, tally, pa, ovf);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW, WIDE>(S, r, h, stk, tally, pa, ovf);
+      scene_trace_min<COUNT, WW, WIDE, TEX>(S, r, h, stk, tally, pa, ovf);
 #endif
       FS_PHASE(2);
       if (h.obj < 0) {
         if (depth == 1) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
         L = mk3(S.sky_r, S.sky_g, S.sky_b);
+        if (TEX && S.sky_tex) {  // textured Light sky: SampleSky (scene.cpp:157-162, engine.cpp:91-92)
+          float tu, tv;
+          sphere_tc(normalize(r.stop - r.start), tu, tv);
+          L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
+        }
         if (depth == 0) {
           f3 nd = normalize(r.dir);
           at_byte(F.normal, pix * 12u)[0] = nd.x;
@@ -1778,9 +1921,14 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       } else {
         f3 p, nn;
         int32_t mi;
-        rebuild_hit(S, r, h, p, nn, mi);
+        float tu, tv;
+        rebuild_hit<TEX>(S, r, h, p, nn, mi, tu, tv, stk);
         if (depth == 1) *at_byte(anchor, a1_off) = make_float4(p.x, p.y, p.z, 0);
         const fs_material& m = S.materials[mi];
+        if (TEX && m.texture >= 0) {
+          f3 tx = sample_tex(S, m, tu, tv);
+          *at_byte(texrow, (depth * kBlock + lane) * 16u) = make_float4(tx.x, tx.y, tx.z, 0.0f);
+        }
         int32_t kind = m.kind;
         f3 view = normalize(p - r.start);
         f3 refl = mat_reflection(S, m, view, nn, rng);
@@ -1827,7 +1975,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         p0 = mk3(a.x, a.y, a.z);
         lp0 = mk3(b.x, b.y, b.z);
       }
-      L = unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane);
+      L = unwind<TEX>(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane, texrow);
       f3 np = mean * (float)n + L;
       float dv = (float)(++n);
       mean = mk3(np.x / dv, np.y / dv, np.z / dv);
@@ -1968,7 +2116,9 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, nodes4, tris, tri_normals, materials, table, counters, pack_send, pack_recv;
+  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send,
+      pack_recv;
+  bool has_textures = false;
   DevScene scene{};
   uint32_t num_objects = 0;
   PreparedScene host;
@@ -2049,9 +2199,9 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 }
 
 // Carves the wavefront state for `slots` paths out of one allocation.
-int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
+int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = false) {
   size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4 +
-               4 * kStackOverflow;
+               4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0);
   size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
   if (ctx->wf.bytes < bytes) {
     int rc = ensure(&ctx->wf, bytes);
@@ -2081,6 +2231,7 @@ int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W) {
   W->list0 = (uint32_t*)take(4ull * slots);
   W->list1 = (uint32_t*)take(4ull * slots);
   W->ovf = (uint32_t*)take(4ull * kStackOverflow * slots);
+  W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
   if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "wavefront state overflow");
   if (!ctx->host_count) FS_HIP(hipHostMalloc((void**)&ctx->host_count, 16, hipHostMallocDefault));
   return FS_OK;
@@ -2188,7 +2339,8 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->materials, &ctx->table,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
+                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
     b->release();
   ctx->wf.release();
@@ -2215,6 +2367,9 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   if ((rc = upload(ctx, &ctx->nodes4, P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node)))) return rc;
   if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri)))) return rc;
   if ((rc = upload(ctx, &ctx->tri_normals, P.tri_normals.data(), P.tri_normals.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->tri_tex, P.tri_tex.data(), P.tri_tex.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->tex_rgb, P.tex_rgb.data(), P.tex_rgb.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->tex_info, P.tex_info.data(), P.tex_info.size() * sizeof(uint32_t)))) return rc;
   if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
   if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
@@ -2227,6 +2382,9 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
   S.table = (const float4*)ctx->table.p;
+  S.tri_tex = (const float2*)ctx->tri_tex.p;
+  S.tex_rgb = (const float*)ctx->tex_rgb.p;
+  S.tex_info = (const uint4*)ctx->tex_info.p;
   S.num_objects = (uint32_t)P.objects.size();
   S.sky = P.sky;
   // Scene::SampleSky (scene.cpp:157-162): LightMaterial emissive x 3; a
@@ -2241,6 +2399,9 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   S.sky_g = sv.y;
   S.sky_b = sv.z;
   S.sky_id = sky.id;
+  S.sky_tex = (sky.kind == FS_MAT_LIGHT && sky.texture >= 0) ? 1 : 0;
+  ctx->has_textures = false;
+  for (const fs_material& m : P.materials) ctx->has_textures |= m.texture >= 0;
   ctx->num_objects = S.num_objects;
   ctx->host = std::move(P);
   ctx->have_scene = true;
@@ -2363,6 +2524,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
   // extend/shade kernels over a compacted path queue.
   const KernelMode mode = kernel_mode();
+  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanBvh4 && mode != KernelMode::kLeanIfIf)
+    return fail(FS_ERR_INVALID, "textured scenes need the default (lean) kernel schedule");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
   if (mode == KernelMode::kWavefront && blocks && params->spp) {
     // Wavefront: begin -> (extend, shade)* until no path is alive.
@@ -2419,7 +2582,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   dev::WfState lean{};
   const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanBvh4 || mode == KernelMode::kLeanIfIf;
   if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
-    if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean))) return rc;
+    if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean, ctx->has_textures))) return rc;
   }
   for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
     L.sample_base = params->sample_base + done;
@@ -2428,12 +2591,15 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     if (mode == KernelMode::kLockstep) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
     if (lean_mode) {
       auto lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
-      if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
+      if (ctx->has_textures)  // textured scenes: the instantiation with texcoords + texel rows
+        lk = count ? dev::render_kernel_lean<true, 6, true, false, true>
+                   : dev::render_kernel_lean<false, 6, true, false, true>;
+      else if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
-      if (mode == KernelMode::kLeanIfIf)
+      else if (mode == KernelMode::kLeanIfIf)
         lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
       hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
-                         lean.p0, lean.ovf, (DevCounters*)ctx->counters.p);
+                         lean.p0, lean.ovf, lean.tex, (DevCounters*)ctx->counters.p);
     } else {
       hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
                          (DevCounters*)ctx->counters.p);

@@ -23,7 +23,11 @@ struct DevScene {
   const float4* __restrict__ tri_normals;
   const fs_material* __restrict__ materials;
   const float4* __restrict__ table;
+  const float* __restrict__ tex_rgb;   // all textures, 3 floats per texel
+  const uint4* __restrict__ tex_info;  // first float, width, height, 0
+  const float2* __restrict__ tri_tex;  // 3 texcoords per triangle (BVH order) or null
   uint32_t num_objects;
+  int32_t sky_tex;  // 1: the sky is a LightMaterial with a map
   int32_t sky;
   float sky_r, sky_g, sky_b;  // Scene::SampleSky value (scene.cpp:157-162), x3 applied
   uint32_t sky_id;

@@ -163,8 +163,15 @@ uint32_t leaf_target_env() {
 class BvhBuilder {
  public:
   BvhBuilder(std::vector<BvhNode>* nodes, std::vector<DevTri>* tris, std::vector<float>* tri_normals,
-             const std::vector<DevTri>* mesh_tris, const std::vector<float>* mesh_normals)
-      : nodes_(nodes), tris_(tris), tri_normals_(tri_normals), mesh_tris_(mesh_tris), mesh_normals_(mesh_normals) {}
+             std::vector<float>* tri_tex, const std::vector<DevTri>* mesh_tris,
+             const std::vector<float>* mesh_normals, const std::vector<float>* mesh_tex)
+      : nodes_(nodes),
+        tris_(tris),
+        tri_normals_(tri_normals),
+        tri_tex_(tri_tex),
+        mesh_tris_(mesh_tris),
+        mesh_normals_(mesh_normals),
+        mesh_tex_(mesh_tex) {}
 
   // Builds the tree over all faces; returns the root node index.
   uint32_t build(std::vector<Prim>& prims, uint32_t* max_depth) {
@@ -230,6 +237,8 @@ class BvhBuilder {
       if (!mesh_normals_->empty())
         tri_normals_->insert(tri_normals_->end(), mesh_normals_->begin() + 12 * (size_t)f,
                              mesh_normals_->begin() + 12 * (size_t)f + 12);
+      if (!mesh_tex_->empty())
+        tri_tex_->insert(tri_tex_->end(), mesh_tex_->begin() + 6 * (size_t)f, mesh_tex_->begin() + 6 * (size_t)f + 6);
     }
     return kLeafBit | ((e - b) << 24) | start;
   }
@@ -325,8 +334,10 @@ class BvhBuilder {
   std::vector<BvhNode>* nodes_;
   std::vector<DevTri>* tris_;
   std::vector<float>* tri_normals_;
+  std::vector<float>* tri_tex_;
   const std::vector<DevTri>* mesh_tris_;
   const std::vector<float>* mesh_normals_;
+  const std::vector<float>* mesh_tex_;
   std::vector<Prim>* prims_ = nullptr;
   uint32_t leaf_ = leaf_target_env();
   uint32_t max_depth_ = 0;
@@ -567,11 +578,34 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       *err = "unknown material kind " + std::to_string(m.kind);
       return FS_ERR_INVALID;
     }
-    if (m.texture >= 0) {
-      *err = "textured materials are not supported by the GPU path yet";
+    if (m.texture >= 0 && (uint32_t)m.texture >= d->num_textures) {
+      *err = "material texture index out of range";
       return FS_ERR_INVALID;
     }
   }
+  // Textures (material.h:42-52): one packed texel array. A map with no texels
+  // is no map (material.cpp:47, 111: buffer.size() && width && height).
+  std::vector<int32_t> tex_slot(d->num_textures, -1);
+  for (uint32_t i = 0; i < d->num_textures; i++) {
+    const fs_texture& t = d->textures[i];
+    size_t n = (size_t)t.width * t.height * 3;
+    if (!n) continue;
+    if (!t.rgb) {
+      *err = "texture " + std::to_string(i) + " has no texels";
+      return FS_ERR_INVALID;
+    }
+    if ((size_t)t.width * t.height * 3 > 0xFFFFFFFFull || S.tex_rgb.size() + n > 0xFFFFFFFFull) {
+      *err = "textures exceed 2^32 floats";
+      return FS_ERR_INVALID;
+    }
+    tex_slot[i] = (int32_t)(S.tex_info.size() / 4);
+    S.tex_info.push_back((uint32_t)S.tex_rgb.size());
+    S.tex_info.push_back(t.width);
+    S.tex_info.push_back(t.height);
+    S.tex_info.push_back(0);
+    S.tex_rgb.insert(S.tex_rgb.end(), t.rgb, t.rgb + n);
+  }
+  for (fs_material& m : S.materials) m.texture = m.texture >= 0 ? tex_slot[m.texture] : -1;
   S.table.resize(4 * (size_t)FS_NORMAL_TABLE_SIZE);
   for (uint32_t i = 0; i < FS_NORMAL_TABLE_SIZE; i++) {
     S.table[4 * i + 0] = d->normal_table[3 * i + 0];
@@ -586,13 +620,16 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     int32_t root4 = -1;
     bool tree = false;
     bool normals = false;
+    bool texcoords = false;
     Bounds rb;
   };
   std::vector<MeshOut> mesh_out(d->num_meshes);
   const bool use4 = bvh4_enabled();
-  bool any_normals = false;
-  for (uint32_t mi = 0; mi < d->num_meshes; mi++)
+  bool any_normals = false, any_tex = false;
+  for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
     if (d->meshes[mi].normals && d->meshes[mi].num_normals) any_normals = true;
+    if (d->meshes[mi].texcoords && d->meshes[mi].num_texcoords) any_tex = true;
+  }
   for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
     const fs_mesh& m = d->meshes[mi];
     if (m.num_triangles && (!m.corners || !m.positions)) {
@@ -638,8 +675,9 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     uint32_t nt = m.texcoords ? m.num_texcoords : 0;
     std::vector<DevTri> mtris(m.num_triangles);
     std::vector<float> corner_pos(need ? 9 * (size_t)m.num_triangles : 0);
-    std::vector<float> mnormals;
+    std::vector<float> mnormals, mtex;
     if (any_normals) mnormals.assign(12 * (size_t)m.num_triangles, 0.0f);
+    if (any_tex) mtex.assign(6 * (size_t)m.num_triangles, 0.0f);
     for (uint32_t f = 0; f < m.num_triangles; f++) {
       const int32_t* c = m.corners + 9 * (size_t)f;
       uint32_t vi[3], ni[3], ti[3];
@@ -672,7 +710,13 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       }
       if (nn)
         for (int k = 0; k < 3; k++) put3(&mnormals[12 * (size_t)f + 4 * k], normals[ni[k]]);
+      if (nt)  // mesh.cpp:236-239, texcoords_ in face (reversed) corner order
+        for (int k = 0; k < 3; k++) {
+          mtex[6 * (size_t)f + 2 * k] = m.texcoords[2 * (size_t)ti[k]];
+          mtex[6 * (size_t)f + 2 * k + 1] = m.texcoords[2 * (size_t)ti[k] + 1];
+        }
     }
+    mesh_out[mi].texcoords = nt > 0;
     mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
     if (!mesh_out[mi].tree) continue;
     if (S.tris.size() + m.num_triangles > kMaxTriangles) {
@@ -689,7 +733,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       p.face = f;
     }
     for (DevTri& t : mtris) t.mesh_obj = mi;
-    BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &mtris, &mnormals);
+    BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex);
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
     if (mesh_out[mi].root == 0xFFFFFFFFu) {
       *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
@@ -719,6 +763,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
       D.i3 = mo.tree ? mo.root4 : -1;
+      D.i4 = mo.texcoords ? 1 : 0;
       put3(D.d, mo.rb.mn);
       put3(D.d + 3, mo.rb.mx);
     } else {

@@ -21,7 +21,8 @@ struct DevObject {
   int32_t i1;    // MESH: 1 if the mesh has vertex normals
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
   int32_t i3;    // MESH: BVH4 root node index, or -1 (traverse the BVH2)
-  int32_t i4, i5;
+  int32_t i4;    // MESH: 1 if the mesh has texcoords (mesh.cpp:300)
+  int32_t i5;
   float d[40];
   // SPHERE  d0-2 center, d3 radius
   // PLANE   d0-3 plane
@@ -92,6 +93,9 @@ struct PreparedScene {
   std::vector<Bvh4Node> nodes4;
   std::vector<DevTri> tris;
   std::vector<float> tri_normals;  // 12 floats per triangle (n0,n1,n2 + pad) or empty
+  std::vector<float> tri_tex;      // 6 floats per triangle (t0,t1,t2) or empty
+  std::vector<float> tex_rgb;      // all textures, 3 floats per texel
+  std::vector<uint32_t> tex_info;  // 4 per texture: first float, width, height, 0
   std::vector<fs_material> materials;
   std::vector<float> table;        // 4 floats per entry
   int32_t sky = 0;

@@ -646,7 +646,11 @@ typedef struct oobj {
   int mesh;
 } oobj;
 
-typedef struct ocoll { float param; v3 point; v3 normal; int mat; int internal; } ocoll; /* object.h:47-61 */
+/* ObjectCollision (object.h:47-61); surface_texcoords default to vector2()
+ * = (0,0) (vector2.cpp:8-11) and are only written by an improving object. */
+typedef struct ocoll { float param; v3 point; v3 normal; int mat; int internal; float tu, tv; } ocoll;
+
+typedef struct otex { float* rgb; uint32_t w, h; } otex; /* Texture (material.h:42-52) */
 
 struct oracle_scene {
   fs_material* mats; uint32_t nmats;
@@ -654,7 +658,43 @@ struct oracle_scene {
   oobj* objs; uint32_t nobjs;
   omesh* meshes; uint32_t nmeshes;
   v3* table; uint32_t ntable;
+  otex* texs; uint32_t ntex;
 };
+
+/* planar_map_texcoords (intersect.cpp:769-778) */
+static inline void planar_map_tc(v3 p, v3 n, float* u, float* v) {
+  if (n.x > n.y && n.x > n.z) { *u = p.y; *v = p.z; return; }
+  if (n.y > n.x && n.y > n.z) { *u = p.x; *v = p.z; return; }
+  *u = p.x; *v = p.y;
+}
+/* sphere_map_texcoords (intersect.cpp:780-784): the float atan2 overload,
+ * BASE_PI is a float (base.h:80), the +0.5 / *0.5 / 1.0- terms are double. */
+static inline void sphere_map(v3 n, float* u, float* v) {
+  float uu = (float)((double)(atan2f(n.x, n.z) / (2 * REF_PI)) + 0.5);
+  float vv = (float)((double)n.y * 0.5 + 0.5);
+  *u = uu;
+  *v = (float)(1.0 - (double)vv);
+}
+/* float -> uint32 as x86-64 compilers lower it (cvttss2si to 64 bits, low
+ * half kept); NaN and |f| >= 2^63 give 0. */
+static inline uint32_t f2u32_x64(float f) {
+  if (!(f > -9.2233715e18f && f < 9.2233715e18f)) return 0;
+  return (uint32_t)(uint64_t)(int64_t)f;
+}
+/* DiffuseMaterial::SampleDiffuse (material.cpp:108-126) */
+static v3 sample_diffuse(const oracle_scene* sc, const fs_material* m, float tu, float tv) {
+  v3 d = mk3(m->diffuse[0], m->diffuse[1], m->diffuse[2]);
+  if (m->texture < 0) return d;
+  const otex* t = &sc->texs[m->texture];
+  if (!t->w || !t->h) return d;
+  float fx = (tu * m->texture_scale * (float)t->w + 0.5f) - 1;
+  float fy = (tv * m->texture_scale * (float)t->h + 0.5f) - 1;
+  uint32_t x = f2u32_x64(fx), y = f2u32_x64(fy);
+  x %= t->w;
+  y %= t->h;
+  uint32_t off = y * t->w * 3 + x * 3;
+  return mk3(t->rgb[off], t->rgb[off + 1], t->rgb[off + 2]);
+}
 
 /* cube::operator=(bounds) + compute_planes (volume.cpp:234-247, 262-283) */
 static void cube_planes(oobj* o) {
@@ -750,6 +790,7 @@ static int build_object(oobj* o, const fs_object* d) {
 
 static inline void take(ocoll* h, const coll_t* c, int mat) {
   h->param = c->param; h->point = c->point; h->normal = c->normal; h->mat = mat;
+  planar_map_tc(c->point, c->normal, &h->tu, &h->tv);  /* object.cpp:67-68, 106-107, 231-232 */
 }
 
 /* Object::Trace implementations (object.cpp:23-237, mesh.cpp:277-322) */
@@ -757,7 +798,11 @@ static int object_trace(const oracle_scene* sc, const oobj* o, const ray_t* r, o
   coll_t t = no_coll();
   switch (o->kind) {
     case FS_OBJ_SPHERE:
-      if (ray_sphere(o->origin, o->radius, r, &t) && t.param < h->param) { take(h, &t, o->mat); return 1; }
+      if (ray_sphere(o->origin, o->radius, r, &t) && t.param < h->param) {
+        take(h, &t, o->mat);
+        sphere_map(t.normal, &h->tu, &h->tv);  /* object.cpp:31 */
+        return 1;
+      }
       return 0;
     case FS_OBJ_PLANE:
       if (ray_plane(o->plane, r, &t) && t.param < h->param) { take(h, &t, o->mat); return 1; }
@@ -779,7 +824,12 @@ static int object_trace(const oracle_scene* sc, const oobj* o, const ray_t* r, o
                 if (plane_dist(o->cplanes[j], ph.point) > 0.0f) { ok = 0; break; }
               }
             }
-            if (ok) { det = 1; take(h, &ph, o->mat); }
+            if (ok) {
+              det = 1;
+              take(h, &ph, o->mat);
+              h->tu = h->tu * 0.1f;  /* object.cpp:157-158: planar map * 0.1f */
+              h->tv = h->tv * 0.1f;
+            }
           }
         }
       }
@@ -808,6 +858,13 @@ static int object_trace(const oracle_scene* sc, const oobj* o, const ray_t* r, o
             v3 n0 = m->normals[f->ni[0]], n1 = m->normals[f->ni[1]], n2 = m->normals[f->ni[2]];
             h->normal = add3(add3(n0, scl3(sub3(n1, n0), mc.bu)), scl3(sub3(n2, n0), mc.bv));
           }
+          if (m->nt) { /* mesh.cpp:300-311: vector2 texcoords interpolated as vector3 */
+            const float* t0 = &m->tex[2 * f->ti[0]];
+            const float* t1 = &m->tex[2 * f->ti[1]];
+            const float* t2 = &m->tex[2 * f->ti[2]];
+            h->tu = (t0[0] + (t1[0] - t0[0]) * mc.bu) + (t2[0] - t0[0]) * mc.bv;
+            h->tv = (t0[1] + (t1[1] - t0[1]) * mc.bu) + (t2[1] - t0[1]) * mc.bv;
+          }
           return 1;
         }
       }
@@ -820,6 +877,7 @@ static int object_trace(const oracle_scene* sc, const oobj* o, const ray_t* r, o
 static int scene_trace(const oracle_scene* sc, const ray_t* r, ocoll* h, tstats* st) {
   int det = 0;
   h->param = 2.0f; h->point = mk3(0, 0, 0); h->normal = mk3(0, 0, 0); h->mat = -1; h->internal = 0;
+  h->tu = h->tv = 0.0f;
   for (uint32_t i = 0; i < sc->nobjs; i++) det |= object_trace(sc, &sc->objs[i], r, h, st);
   v4 cp = plane_np(h->normal, h->point);
   if (plane_dist(cp, r->start) < 0.0) {
@@ -889,14 +947,17 @@ static int mat_will_use_indirect(const fs_material* m, v3 r, v3 n) {
 }
 static inline v3 mat_diffuse(const fs_material* m) { return mk3(m->diffuse[0], m->diffuse[1], m->diffuse[2]); }
 
-/* Material::Sample (material.cpp:43-339); textures are not restated in round 1. */
-static v3 mat_sample(const fs_material* m, uint32_t depth, v3 sample_pos, v3 view_dir, v3 light_pos, v3 light_dir,
-                     v3 light_color, v3 n, uint64_t* rng) {
+/* Material::Sample (material.cpp:43-339). SampleDiffuse is used by Light
+ * (textured only), Diffuse, Metal, Ceramic and Glow. */
+static v3 mat_sample(const oracle_scene* sc, const fs_material* m, uint32_t depth, v3 sample_pos, v3 view_dir,
+                     v3 light_pos, v3 light_dir, v3 light_color, v3 n, float tu, float tv, uint64_t* rng) {
   switch (m->kind) {
-    case FS_MAT_LIGHT: return mk3(m->emissive[0], m->emissive[1], m->emissive[2]);
-    case FS_MAT_DIFFUSE: return scl3(mul3(mat_diffuse(m), light_color), fmaxf(0.0f, dot3(n, light_dir)));
+    case FS_MAT_LIGHT:
+      if (m->texture >= 0 && sc->texs[m->texture].w && sc->texs[m->texture].h) return sample_diffuse(sc, m, tu, tv);
+      return mk3(m->emissive[0], m->emissive[1], m->emissive[2]);
+    case FS_MAT_DIFFUSE: return scl3(mul3(sample_diffuse(sc, m, tu, tv), light_color), fmaxf(0.0f, dot3(n, light_dir)));
     case FS_MAT_METAL: {
-      v3 d = mat_diffuse(m);
+      v3 d = sample_diffuse(sc, m, tu, tv);
       v3 dc = scl3(mul3(d, light_color), fmaxf(0.0f, dot3(n, light_dir)));
       v3 rc = mul3(d, light_color);
       return add3(scl3(dc, m->roughness), scl3(rc, (float)(1.0 - (double)m->roughness)));
@@ -907,7 +968,7 @@ static v3 mat_sample(const fs_material* m, uint32_t depth, v3 sample_pos, v3 vie
     case FS_MAT_CERAMIC:
     case FS_MAT_GLOW: {
       v3 h = norm3(add3(scl3(view_dir, (float)-1.0), light_dir));
-      v3 dc = scl3(mul3(mat_diffuse(m), light_color), fmaxf(0.0f, dot3(n, light_dir)));
+      v3 dc = scl3(mul3(sample_diffuse(sc, m, tu, tv), light_color), fmaxf(0.0f, dot3(n, light_dir)));
       float ds = (float)pow((double)dot3(h, n), 50);
       v3 out = add3(scl3(light_color, ds), scl3(dc, (float)(1.0 - (double)ds)));
       if (m->kind == FS_MAT_GLOW) out = add3(out, mk3(m->glow[0], m->glow[1], m->glow[2]));
@@ -928,12 +989,22 @@ static v3 mat_sample(const fs_material* m, uint32_t depth, v3 sample_pos, v3 vie
 
 /* Scene::SampleSky (scene.cpp:157-162) with the scene.cpp:383 static cast:
  * a non-Light sky dispatches to its own Sample with black light -> 0 (Glow
- * keeps its glow term). Textured skies are not restated in round 1. */
-static v3 sample_sky(const oracle_scene* sc) {
+ * keeps its glow term). A textured Light sky samples its map at the sphere
+ * map of the normalised segment direction (engine.cpp:91-92). */
+static v3 sample_sky(const oracle_scene* sc, v3 view) {
   const fs_material* m = &sc->mats[sc->sky];
   v3 out = mk3(0, 0, 0);
-  if (m->kind == FS_MAT_LIGHT) out = mk3(m->emissive[0], m->emissive[1], m->emissive[2]);
-  else if (m->kind == FS_MAT_GLOW) out = mk3(m->glow[0], m->glow[1], m->glow[2]);
+  if (m->kind == FS_MAT_LIGHT) {
+    if (m->texture >= 0 && sc->texs[m->texture].w && sc->texs[m->texture].h) {
+      float u, v;
+      sphere_map(view, &u, &v);
+      out = sample_diffuse(sc, m, u, v);
+    } else {
+      out = mk3(m->emissive[0], m->emissive[1], m->emissive[2]);
+    }
+  } else if (m->kind == FS_MAT_GLOW) {
+    out = mk3(m->glow[0], m->glow[1], m->glow[2]);
+  }
   return scl3(out, (float)3.0);
 }
 
@@ -951,7 +1022,7 @@ static v3 trace_step(const oracle_scene* sc, const fs_camera* cam, const ray_t* 
   if (st) st->segs++;
   if (!scene_trace(sc, r, &ci, st)) {
     if (hit_position) *hit_position = r->stop;
-    v3 out = sample_sky(sc);
+    v3 out = sample_sky(sc, norm3(sub3(r->stop, r->start)));
     if (depth == 0) {
       res->color = out;
       res->normal = norm3(r->dir);
@@ -972,7 +1043,7 @@ static v3 trace_step(const oracle_scene* sc, const fs_camera* cam, const ray_t* 
   if (mat_will_use_indirect(m, refl, ci.normal)) {
     ind = trace_step(sc, cam, &rr, &ind_origin, depth + 1, res, rng, st);
   }
-  v3 out = mat_sample(m, depth, ci.point, view, ind_origin, refl, ind, ci.normal, rng);
+  v3 out = mat_sample(sc, m, depth, ci.point, view, ind_origin, refl, ind, ci.normal, ci.tu, ci.tv, rng);
   if (depth == 0) {
     if (len3(out) > 10.0 && m->kind == FS_MAT_LIGHT) out = scl3(norm3(out), (float)10.0);
     res->color = out;
@@ -1071,9 +1142,22 @@ int oracle_scene_create(const fs_scene_desc* d, oracle_scene** out) {
   s->table = (v3*)malloc(sizeof(v3) * s->ntable);
   for (uint32_t i = 0; i < s->ntable; i++)
     s->table[i] = mk3(d->normal_table[3 * i], d->normal_table[3 * i + 1], d->normal_table[3 * i + 2]);
+  int rc = 0;
+  s->ntex = d->num_textures;
+  s->texs = (otex*)calloc(s->ntex ? s->ntex : 1, sizeof(otex));
+  for (uint32_t i = 0; i < s->ntex; i++) {
+    const fs_texture* t = &d->textures[i];
+    size_t n = (size_t)t->width * t->height * 3;
+    if (n && !t->rgb) rc = FS_ERR_INVALID;
+    s->texs[i].w = t->width;
+    s->texs[i].h = t->height;
+    s->texs[i].rgb = (float*)malloc(sizeof(float) * (n ? n : 1));
+    if (n && t->rgb) memcpy(s->texs[i].rgb, t->rgb, sizeof(float) * n);
+  }
+  for (uint32_t i = 0; i < s->nmats; i++)
+    if (s->mats[i].texture >= 0 && (uint32_t)s->mats[i].texture >= s->ntex) rc = FS_ERR_INVALID;
   s->nmeshes = d->num_meshes;
   s->meshes = (omesh*)calloc(s->nmeshes ? s->nmeshes : 1, sizeof(omesh));
-  int rc = 0;
   for (uint32_t i = 0; i < s->nmeshes && !rc; i++) rc = mesh_build(&s->meshes[i], &d->meshes[i]);
   s->nobjs = d->num_objects;
   s->objs = (oobj*)calloc(s->nobjs ? s->nobjs : 1, sizeof(oobj));
@@ -1091,7 +1175,8 @@ int oracle_scene_create(const fs_scene_desc* d, oracle_scene** out) {
 void oracle_scene_destroy(oracle_scene* s) {
   if (!s) return;
   for (uint32_t i = 0; i < s->nmeshes; i++) mesh_free(&s->meshes[i]);
-  free(s->meshes); free(s->objs); free(s->mats); free(s->table); free(s);
+  for (uint32_t i = 0; i < s->ntex; i++) free(s->texs[i].rgb);
+  free(s->texs); free(s->meshes); free(s->objs); free(s->mats); free(s->table); free(s);
 }
 
 int oracle_mesh_info(const oracle_scene* s, uint32_t mesh, uint32_t* nodes, uint64_t* refs, float* rb) {

@@ -15,11 +15,23 @@ class DescBuilder:
         self.mats = []
         self.objs = []
         self.meshes = []
+        self.textures = []
         self._keep = []
         self.sky = self.material(fsamd.MAT_LIGHT, emissive=(0, 0, 0))  # Scene::Scene sky
 
+    def texture(self, rgb):
+        """A diffuse map (Texture, material.h:42-52): H x W x 3 floats, rows as loaded."""
+        a = np.ascontiguousarray(rgb, np.float32)
+        t = fsamd.fs_texture()
+        t.rgb = a.ctypes.data_as(C.POINTER(C.c_float))
+        t.height, t.width = a.shape[0], a.shape[1]
+        self._keep.append(a)
+        self.textures.append(t)
+        return len(self.textures) - 1
+
     def material(self, kind, diffuse=(0, 0, 0), emissive=(0, 0, 0), glow=(0, 0, 0), roughness=0.5,
-                 shininess=0.0, index=0.75, reflectivity=0.1, frost=0.0, density=0.0):
+                 shininess=0.0, index=0.75, reflectivity=0.1, frost=0.0, density=0.0, texture=-1,
+                 texture_scale=1.0):
         m = fsamd.fs_material()
         m.kind = kind
         m.id = fsamd.random_integer() & 0xFFFFFFFF
@@ -28,8 +40,8 @@ class DescBuilder:
         m.glow[:] = glow
         m.roughness, m.shininess, m.index, m.reflectivity, m.frost = roughness, shininess, index, reflectivity, frost
         m.density = density * 1000.0  # FogMaterial ctor (material.cpp:306)
-        m.texture = -1
-        m.texture_scale = 0.0
+        m.texture = texture
+        m.texture_scale = texture_scale if texture >= 0 else 0.0
         self.mats.append(m)
         return len(self.mats) - 1
 
@@ -42,13 +54,15 @@ class DescBuilder:
         return len(self.objs) - 1
 
     def mesh(self, mat, positions, faces, normals=None, corner_normals=None, invert=False,
-             translation=(0, 0, 0), scale=(1, 1, 1), rotation=(0, 0, 0, 0)):
+             translation=(0, 0, 0), scale=(1, 1, 1), rotation=(0, 0, 0, 0), texcoords=None, corner_tex=None):
         pos = np.ascontiguousarray(positions, np.float32)
         faces = np.asarray(faces, np.int32)
         corners = np.full((len(faces), 9), -1, np.int32)
         corners[:, 0::3] = faces
         if corner_normals is not None:
             corners[:, 1::3] = np.asarray(corner_normals, np.int32)
+        if corner_tex is not None:
+            corners[:, 2::3] = np.asarray(corner_tex, np.int32)
         corners = np.ascontiguousarray(corners)
         m = fsamd.fs_mesh()
         m.positions = pos.ctypes.data_as(C.POINTER(C.c_float))
@@ -58,6 +72,11 @@ class DescBuilder:
             m.normals = nrm.ctypes.data_as(C.POINTER(C.c_float))
             m.num_normals = len(nrm)
             self._keep.append(nrm)
+        if texcoords is not None:
+            tc = np.ascontiguousarray(texcoords, np.float32)
+            m.texcoords = tc.ctypes.data_as(C.POINTER(C.c_float))
+            m.num_texcoords = len(tc)
+            self._keep.append(tc)
         m.corners = corners.ctypes.data_as(C.POINTER(C.c_int32))
         m.num_triangles = len(faces)
         m.invert_normals = int(invert)
@@ -82,6 +101,10 @@ class DescBuilder:
         d.num_objects = len(self.objs)
         d.meshes = C.cast(self._meshes, C.POINTER(fsamd.fs_mesh))
         d.num_meshes = len(self.meshes)
+        if self.textures:
+            self._texs = (fsamd.fs_texture * len(self.textures))(*self.textures)
+            d.textures = C.cast(self._texs, C.POINTER(fsamd.fs_texture))
+            d.num_textures = len(self.textures)
         d.normal_table = self.table.ctypes.data_as(C.POINTER(C.c_float))
         self.desc = d
         return C.cast(C.pointer(d), C.c_void_p)

@@ -180,6 +180,85 @@ def test_empty_scene_is_all_sky(gpu_renderer):
         np.float32([0.75, 1.5, 3.0]), (16, 16, 3)))
 
 
+# ---- textures (material.cpp:108-126, object.cpp texcoords, mesh.cpp:300-311) -
+def textured_scene(spheres):
+    """Textured Diffuse/Metal/Ceramic/Glow/Light on planar-mapped objects and
+    meshes with texcoords; a texcoord-less mesh after a planar writer (the
+    reference keeps the earlier surface_texcoords); negative and scaled
+    coordinates; non-power-of-two maps. With spheres=True also sphere-mapped
+    spheres and a textured Light sky (atan2f: tolerance)."""
+    rng = np.random.default_rng(7)
+    b = DescBuilder()
+    t0 = b.texture(rng.random((23, 37, 3)))
+    t1 = b.texture(rng.random((64, 64, 3)) * 0.9 + 0.05)
+    t2 = b.texture(rng.random((5, 3, 3)) * 4.0)  # HDR-ish emitter
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(15, 15, 15))
+    tdiff = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.5, 0.5, 0.5), texture=t0, texture_scale=0.37)
+    tmetal = b.material(fsamd.MAT_METAL, diffuse=(0.9, 0.8, 0.6), roughness=0.4, texture=t1, texture_scale=0.11)
+    tcer = b.material(fsamd.MAT_CERAMIC, diffuse=(0.8, 0.8, 0.8), shininess=0.6, texture=t1, texture_scale=2.5)
+    tglow = b.material(fsamd.MAT_GLOW, diffuse=(0.5, 0.5, 0.5), glow=(0.1, 0.05, 0.0), shininess=0.4, texture=t0)
+    tlight = b.material(fsamd.MAT_LIGHT, emissive=(9, 9, 9), texture=t2, texture_scale=0.5)
+    tmirror = b.material(fsamd.MAT_MIRROR, diffuse=(0.9, 0.9, 0.9), texture=t0)  # map unused by Mirror
+    cornell_room(b, white, red, light)
+    b.obj(fsamd.OBJ_PLANE, tdiff, [0, 1, 0, -0.25])                   # floor, planar (x, z)
+    b.obj(fsamd.OBJ_QUAD_ONWH, tglow, [-8, 5, 5, 1, 0, 0.2, 4, 6])
+    b.obj(fsamd.OBJ_QUAD_ONWH, tlight, [6, 12, 8, -1, -0.3, -1, 3, 3])
+    b.obj(fsamd.OBJ_DISC, tmetal, [0, 0.5, 0, 0, 1, 0, 3])
+    b.obj(fsamd.OBJ_CUBOID, tmetal, [4, 2, -4, 3, 4, 3, 0, 1, 0, 0.5], rotate=1)   # texcoords * 0.1
+    b.obj(fsamd.OBJ_QUAD_PUV, tmirror, [-9, 1, 9, 0, 6, 0, 4, 0, 0])
+    # a mesh with texcoords (negative u/v too)
+    mv = [[-6, 2, -2], [-2, 2, -2], [-2, 8, -2], [-6, 8, -2]]
+    b.mesh(tcer, mv, [[0, 1, 2], [0, 2, 3]], texcoords=[[-1.3, 0.2], [2.7, -0.4], [1.1, 3.3], [-0.6, 1.9]],
+           corner_tex=[[0, 1, 2], [0, 2, 3]], translation=(0, 0, 1e-3))
+    # a large quad behind, then a texcoord-less textured mesh in front of part of it:
+    # its hits keep the quad's planar texcoords (reference hit_info reuse)
+    b.obj(fsamd.OBJ_QUAD_ONWH, white, [2, 10, 9.5, 0, 0, -1, 12, 12])
+    b.mesh(tdiff, [[0, 6, 9], [6, 6, 9], [6, 14, 9]], [[0, 1, 2]], translation=(0, 0, 1e-3))
+    # a texcoord-less textured mesh in front of texcoord-less walls only: the
+    # texcoords stay vector2() = (0, 0)
+    b.mesh(tdiff, [[-9, 14, 9], [-6, 14, 9], [-6, 18, 9]], [[0, 1, 2]], translation=(0, 0, 1e-3))
+    if spheres:
+        b.obj(fsamd.OBJ_SPHERE, tcer, [-4, 5, -3, 2])
+        b.obj(fsamd.OBJ_SPHERE, tdiff, [5, 12, 2, 2])
+        sky = b.material(fsamd.MAT_LIGHT, emissive=(0.2, 0.2, 0.2), texture=t1, texture_scale=1.0)
+        b.sky = sky
+    return b
+
+
+def test_textures_planar_and_mesh_bit_exact(gpu_renderer):
+    b = textured_scene(spheres=False)
+    ptr = b.build()
+    out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    ref = oracle_render(ptr, CAM, 96, 72, 16)
+    assert_parity(out, ref, exact=True)
+    # the maps are actually sampled: differs from the same scene without them
+    for m in b.mats:
+        m.texture = -1
+    plain = gpu_render(gpu_renderer, b.build(), CAM, 96, 72, 16)
+    assert not np.array_equal(plain[fsamd.PLANE_COLOR], out[fsamd.PLANE_COLOR])
+
+
+def test_textures_sphere_map_and_sky_within_tolerance(gpu_renderer):
+    # sphere_map_texcoords calls atan2f (ocml here, the C runtime in the reference)
+    b = textured_scene(spheres=True)
+    ptr = b.build()
+    out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    ref = oracle_render(ptr, CAM, 96, 72, 16)
+    assert_parity(out, ref, exact=False)
+
+
+def test_textured_scene_rejects_other_schedules(gpu_renderer, monkeypatch):
+    b = textured_scene(spheres=False)
+    gpu_renderer.upload(b.build())
+    f = gpu_renderer.frame(16, 16)
+    monkeypatch.setenv("FS_KERNEL", "lockstep")
+    with pytest.raises(RuntimeError):
+        gpu_renderer.render(CAM, f, spp=1)
+    f.close()
+
+
 # ---- size-independent properties at full size ------------------------------
 def test_full_size_properties(scene_dir, gpu_renderer):
     """1080p: chunking, sharding and determinism invariants, plus per-sample
