@@ -129,6 +129,11 @@ HOST_SYMBOLS = {
     "fsh_obj_info": ([_VP] + [C.POINTER(C.c_uint32)] * 4, C.c_int),
     "fsh_obj_copy": ([_VP, _VP, _VP], C.c_int),
     "fsh_obj_free": ([_VP], None),
+    "fsh_load_bitmap": ([C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_uint32),
+                         C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)], C.c_int),
+    "fsh_load_exr": ([C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_int), C.POINTER(C.c_int)],
+                     C.c_int),
+    "fsh_free": ([_VP], None),
 }
 
 _gpu = None
@@ -389,3 +394,31 @@ class Renderer:
         if self.ctx:
             gpu_lib().fs_destroy(self.ctx)
             self.ctx = None
+
+
+def load_bitmap(path):
+    """LoadBitmap (bitmap.cpp:40-104) through the host library: (ok, width,
+    height, texels) with texels an (n,) float32 array as the loader left it."""
+    lib = host_lib()
+    buf = C.POINTER(C.c_float)()
+    w, h, n = C.c_uint32(), C.c_uint32(), C.c_size_t()
+    ok = lib.fsh_load_bitmap(str(path).encode(), C.byref(buf), C.byref(w), C.byref(h), C.byref(n))
+    try:
+        arr = np.ctypeslib.as_array(buf, shape=(max(n.value, 1),))[:n.value].copy()
+    finally:
+        lib.fsh_free(buf)
+    return bool(ok), w.value, h.value, arr
+
+
+def load_exr(path):
+    """tinyexr LoadEXR restatement: (H, W, 4) float32 RGBA; raises FsError."""
+    lib = host_lib()
+    buf = C.POINTER(C.c_float)()
+    w, h = C.c_int(), C.c_int()
+    rc = lib.fsh_load_exr(str(path).encode(), C.byref(buf), C.byref(w), C.byref(h))
+    if rc:
+        raise FsError(f"LoadEXR failed ({rc}): {lib.fsh_last_error().decode(errors='replace')}")
+    try:
+        return np.ctypeslib.as_array(buf, shape=(h.value * w.value * 4,)).reshape(h.value, w.value, 4).copy()
+    finally:
+        lib.fsh_free(buf)

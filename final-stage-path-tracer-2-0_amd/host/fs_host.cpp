@@ -1,6 +1,7 @@
 // fs_host.cpp — the reference render API (namespace base) on top of the
 // MI355X path-trace layer. See fs_host.h for the mapping.
 #include "fs_host.h"
+#include "fs_image.h"
 
 #include <chrono>
 #include <cmath>
@@ -56,12 +57,33 @@ static bool ends_with(const std::string& s, const std::string& e) {
 
 DiffuseMaterial::DiffuseMaterial(const vector3& diffuse) : texture_scale_(0) { diffuse_ = diffuse; }
 DiffuseMaterial::DiffuseMaterial(const std::string& filename, float32 tex_scale) : texture_scale_(0) {
+  diffuse_map_.filename = filename;
   LoadDiffuseTexture(filename, tex_scale);
 }
-void DiffuseMaterial::LoadDiffuseTexture(const std::string& filename, float32 tex_scale) {
+void DiffuseMaterial::LoadDiffuseTexture(const std::string& filename, float32 tex_scale) {  // material.cpp:63-95
+  diffuse_map_.filename = filename;
   texture_scale_ = tex_scale;
-  // material.cpp:63-95: only .bmp / .exr files that load become a texture.
-  if ((ends_with(filename, ".bmp") || ends_with(filename, ".exr")) && file_exists(filename)) texture_file_ = filename;
+  if (ends_with(filename, ".bmp")) {
+    LoadBitmap(filename, &diffuse_map_.buffer, &diffuse_map_.width, &diffuse_map_.height);
+  } else if (ends_with(filename, ".exr")) {
+    float* rgba = nullptr;
+    const char* errors = nullptr;
+    int width, height;
+    if (LoadEXR(&rgba, &width, &height, filename.c_str(), &errors) < 0) {
+      std::printf("Failed to load %s. Errors: %s.\n", filename.c_str(), errors ? errors : "");
+      return;
+    }
+    std::printf("Loaded %s with dims: <%i, %i>.\n", filename.c_str(), width, height);
+    diffuse_map_.width = (uint32)width;
+    diffuse_map_.height = (uint32)height;
+    diffuse_map_.buffer.resize((size_t)width * height * 3);
+    for (size_t i = 0; i < (size_t)width * height; i++) {
+      diffuse_map_.buffer[i * 3 + 0] = rgba[i * 4 + 0];
+      diffuse_map_.buffer[i * 3 + 1] = rgba[i * 4 + 1];
+      diffuse_map_.buffer[i * 3 + 2] = rgba[i * 4 + 2];
+    }
+    std::free(rgba);
+  }
 }
 fs_material DiffuseMaterial::Base(int kind) const {
   fs_material m;
@@ -71,7 +93,7 @@ fs_material DiffuseMaterial::Base(int kind) const {
   m.diffuse[0] = diffuse_.x;
   m.diffuse[1] = diffuse_.y;
   m.diffuse[2] = diffuse_.z;
-  m.texture = texture_file_.empty() ? -1 : 0;
+  m.texture = -1;  // assigned by Scene::Describe
   m.texture_scale = texture_scale_;
   return m;
 }
@@ -650,6 +672,7 @@ const fs_scene_desc* Scene::Describe(std::string* err) {
   desc_mats_.clear();
   desc_objs_.clear();
   desc_meshes_.clear();
+  desc_tex_.clear();
   std::map<Material*, int32> index;
   auto mat_index = [&](const std::shared_ptr<Material>& m) -> int32 {
     if (!m) return -1;
@@ -658,7 +681,14 @@ const fs_scene_desc* Scene::Describe(std::string* err) {
     int32 i = (int32)desc_mats_.size();
     index[m.get()] = i;
     desc_mat_ptrs_.push_back(m);
-    desc_mats_.push_back(m->Describe());
+    fs_material d = m->Describe();
+    auto* dm = dynamic_cast<const DiffuseMaterial*>(m.get());
+    if (dm && dm->HasDiffuseMap()) {
+      const Texture& t = dm->diffuse_map();
+      d.texture = (int32)desc_tex_.size();
+      desc_tex_.push_back(fs_texture{t.buffer.data(), t.width, t.height});
+    }
+    desc_mats_.push_back(d);
     return i;
   };
   int32 sky = mat_index(sky_material_);
@@ -685,6 +715,8 @@ const fs_scene_desc* Scene::Describe(std::string* err) {
   desc_.num_objects = (uint32_t)desc_objs_.size();
   desc_.meshes = desc_meshes_.empty() ? nullptr : desc_meshes_.data();
   desc_.num_meshes = (uint32_t)desc_meshes_.size();
+  desc_.textures = desc_tex_.empty() ? nullptr : desc_tex_.data();
+  desc_.num_textures = (uint32_t)desc_tex_.size();
   desc_.normal_table = g_normal_table.data();
   return &desc_;
 }
@@ -910,5 +942,26 @@ int fsh_obj_copy(void* h, float* positions, int32_t* corners) {
   return FS_OK;
 }
 void fsh_obj_free(void* h) { delete static_cast<base::MeshData*>(h); }
+
+// Texture loaders (host/fs_image.h), for tests. fsh_load_bitmap returns
+// LoadBitmap's result and hands back whatever it left in the buffer (n floats).
+int fsh_load_bitmap(const char* path, float** out, uint32_t* w, uint32_t* h, size_t* n) {
+  std::vector<float> buf;
+  uint32_t ww = 0, hh = 0;
+  bool ok = base::LoadBitmap(path ? path : "", &buf, &ww, &hh);
+  *out = static_cast<float*>(std::malloc(sizeof(float) * (buf.size() ? buf.size() : 1)));
+  if (buf.size()) std::memcpy(*out, buf.data(), sizeof(float) * buf.size());
+  *w = ww;
+  *h = hh;
+  *n = buf.size();
+  return ok ? 1 : 0;
+}
+int fsh_load_exr(const char* path, float** rgba, int* w, int* h) {
+  const char* err = nullptr;
+  int rc = base::LoadEXR(rgba, w, h, path, &err);
+  if (rc) g_host_error = err ? err : "LoadEXR failed";
+  return rc;
+}
+void fsh_free(void* p) { std::free(p); }
 
 }  // extern "C"

@@ -69,20 +69,31 @@ class Material {
   uint32 material_id_;
 };
 
+// Texture (material.h:42-52): RGB floats, rows in file order.
+struct Texture {
+  std::string filename;
+  std::vector<float32> buffer;
+  uint32 width = 0;
+  uint32 height = 0;
+};
+
 class DiffuseMaterial : public Material {
  public:
   DiffuseMaterial() : texture_scale_(0) {}
   explicit DiffuseMaterial(const vector3& diffuse);
   DiffuseMaterial(const std::string& filename, float32 tex_scale = 1.0f);
-  // Records the texture; textured materials are rejected by the GPU path in
-  // this round (fs_upload_scene returns FS_ERR_INVALID).
+  // material.cpp:63-95: .bmp through LoadBitmap, .exr through LoadEXR
+  // (host/fs_image.h); any other extension leaves the map empty.
   void LoadDiffuseTexture(const std::string& filename, float32 tex_scale = 1.0f);
   fs_material Describe() const override;
+  // material.cpp:111: a map is used only when it holds texels.
+  bool HasDiffuseMap() const { return diffuse_map_.buffer.size() && diffuse_map_.width && diffuse_map_.height; }
+  const Texture& diffuse_map() const { return diffuse_map_; }
 
  protected:
   fs_material Base(int kind) const;
   vector3 diffuse_;
-  std::string texture_file_;
+  Texture diffuse_map_;
   float32 texture_scale_;
 };
 
@@ -325,6 +336,7 @@ class Scene {
   std::vector<fs_material> desc_mats_;
   std::vector<fs_object> desc_objs_;
   std::vector<fs_mesh> desc_meshes_;
+  std::vector<fs_texture> desc_tex_;
   fs_scene_desc desc_{};
 };
 
