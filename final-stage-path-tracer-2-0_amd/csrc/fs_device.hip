@@ -964,6 +964,7 @@ struct WfState {
   uint32_t* list1;
   uint32_t* ovf;    // lean megakernel: BVH4 stack overflow rows
   float4* tex;      // lean megakernel: per-level texel rows (textured scenes)
+  float* rad;       // lean megakernel (pooled): per-sample radiance rows
   uint32_t* count;  // [0], [1]: active counts
 };
 
@@ -1812,12 +1813,13 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false>
+template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false, bool POOL = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
                                                                      uint32_t* __restrict__ ovf_all,
                                                                      float4* __restrict__ tex_all,
+                                                                     float* __restrict__ rad_all,
                                                                      DevCounters* __restrict__ counters) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
   const uint32_t lane = threadIdx.x;
@@ -1830,22 +1832,40 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   uint32_t* ovf = ovf_all + (size_t)blockIdx.x * (kStackOverflow * kBlock) + lane;
   float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
 
-  uint32_t x, y;
+  uint32_t x0, y0;  // the wave's 8x8 pixel micro-tile
   {
     const uint32_t micro_per_side = P.tile_size / 8;
     const uint32_t micro_per_tile = micro_per_side * micro_per_side;
     const uint32_t owned = blockIdx.x / micro_per_tile, micro = blockIdx.x % micro_per_tile;
     const uint32_t tile = P.tile_offset + owned * P.tile_stride;
     const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
-    y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+    x0 = tx * P.tile_size + (micro % micro_per_side) * 8;
+    y0 = ty * P.tile_size + (micro / micro_per_side) * 8;
   }
-  if (x >= F.width || y >= F.height) return;
-  const uint32_t pix = y * F.width + x;
-  f3 mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
-  uint32_t n = F.count[pix];
+  uint32_t x = x0 + (lane & 7), y = y0 + (lane >> 3);
+  const bool own_valid = x < F.width && y < F.height;
+  if (!POOL && !own_valid) return;
+  if (POOL && (x0 >= F.width || y0 >= F.height)) return;  // whole micro-tile outside the frame
+  uint32_t pix = y * F.width + x;
+  f3 mean = mk3(0, 0, 0);
+  uint32_t n = 0;
+  if (!POOL) {
+    mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
+    n = F.count[pix];
+  }
   Tally<COUNT> tally;
   uint32_t segments = 0;
+  // POOL: the wave's kBlock x spp (pixel, sample) tasks are taken in
+  // sample-major order from a wave-uniform counter by whichever lane is
+  // free; each sample's radiance goes to a scratch row and every pixel folds
+  // its samples in order at the end (same running-mean rounding).
+  float* rad = rad_all + (size_t)blockIdx.x * (3 * kChunk * kBlock);
+  uint32_t next_task = 0;
+  // only the micro-tile's in-frame pixels (vx x vy) are enumerated, so every
+  // task is real work and the loop has no early continue
+  const uint32_t vx = min(8u, F.width - x0), vy = min(8u, F.height - y0), nvalid = vx * vy;
+  const uint32_t total_tasks = nvalid * P.spp;
+  uint32_t task_lp = lane;
 
   uint32_t s = 0;
   uint64_t rng = 0;
@@ -1867,8 +1887,24 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   do {              \
   } while (0)
 #endif
-  while (s < P.spp) {
+  for (;;) {
+    if (!POOL && s >= P.spp) break;
     FS_PHASE(0);
+    if (POOL) {
+      const uint64_t m = __ballot(fresh);
+      if (fresh) {
+        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        uint32_t task = next_task + rank;
+        if (task >= total_tasks) break;  // this lane is done
+        s = task / nvalid;
+        const uint32_t k = task - s * nvalid, px = k % vx, py = k / vx;
+        task_lp = py * 8 + px;
+        x = x0 + px;
+        y = y0 + py;
+        pix = y * F.width + x;
+      }
+      next_task += (uint32_t)__popcll(m);
+    }
     if (fresh) {
       rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
       r = camera_ray(C, (float)x, (float)y, rng);
@@ -1909,7 +1945,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           sphere_tc(normalize(r.stop - r.start), tu, tv);
           L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
         }
-        if (depth == 0) {
+        if (depth == 0 && (!POOL || s == P.spp - 1)) {  // the last sample's AOVs remain
           f3 nd = normalize(r.dir);
           at_byte(F.normal, pix * 12u)[0] = nd.x;
           at_byte(F.normal, pix * 12u)[1] = nd.y;
@@ -1944,8 +1980,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         else
           mats_hi |= (uint32_t)mi << (8 * (depth - 4));
         top = (int)depth;
-        if (depth == 0) {
-          *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
+        if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
+        if (depth == 0 && (!POOL || s == P.spp - 1)) {
           at_byte(F.normal, pix * 12u)[0] = nn.x;
           at_byte(F.normal, pix * 12u)[1] = nn.y;
           at_byte(F.normal, pix * 12u)[2] = nn.z;
@@ -1976,10 +2012,17 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX>(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      f3 np = mean * (float)n + L;
-      float dv = (float)(++n);
-      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-      s++;
+      if (POOL) {
+        const uint32_t o = s * kBlock + task_lp;
+        rad[o] = L.x;
+        rad[kChunk * kBlock + o] = L.y;
+        rad[2 * kChunk * kBlock + o] = L.z;
+      } else {
+        f3 np = mean * (float)n + L;
+        float dv = (float)(++n);
+        mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+        s++;
+      }
       fresh = true;
     }
     FS_PHASE(4);
@@ -1993,6 +2036,22 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     for (int i = 0; i < 10; i++) atomicAdd(&counters->phase[i], (unsigned long long)ph[i]);
 #endif
 #undef FS_PHASE
+  if (POOL) {
+    __syncthreads();  // the wave's radiance rows are complete and visible
+    if (!own_valid) return;
+    x = x0 + (lane & 7);
+    y = y0 + (lane >> 3);
+    pix = y * F.width + x;
+    mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
+    n = F.count[pix];
+    for (uint32_t k = 0; k < P.spp; k++) {  // frame.cpp:53-63, samples in order
+      const uint32_t o = k * kBlock + lane;
+      f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
+      f3 np = mean * (float)n + L;
+      float dv = (float)(++n);
+      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+    }
+  }
   F.color[3 * (size_t)pix] = mean.x;
   F.color[3 * (size_t)pix + 1] = mean.y;
   F.color[3 * (size_t)pix + 2] = mean.z;
@@ -2201,7 +2260,7 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 // Carves the wavefront state for `slots` paths out of one allocation.
 int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = false) {
   size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4 +
-               4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0);
+               4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
   size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
   if (ctx->wf.bytes < bytes) {
     int rc = ensure(&ctx->wf, bytes);
@@ -2232,6 +2291,7 @@ int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = f
   W->list1 = (uint32_t*)take(4ull * slots);
   W->ovf = (uint32_t*)take(4ull * kStackOverflow * slots);
   W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
+  W->rad = (float*)take(12ull * kChunk * slots);
   if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "wavefront state overflow");
   if (!ctx->host_count) FS_HIP(hipHostMalloc((void**)&ctx->host_count, 16, hipHostMallocDefault));
   return FS_OK;
@@ -2286,7 +2346,7 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   return FS_OK;
 }
 
-enum class KernelMode { kLean, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
+enum class KernelMode { kLean, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
 
 KernelMode kernel_mode() {
   const char* e = std::getenv("FS_KERNEL");
@@ -2295,6 +2355,7 @@ KernelMode kernel_mode() {
   if (m == "regen") return KernelMode::kRegen;
   if (m == "lean_ifif") return KernelMode::kLeanIfIf;
   if (m == "lean_bvh4") return KernelMode::kLeanBvh4;
+  if (m == "lean_nopool") return KernelMode::kLeanNoPool;
   if (m == "lockstep") return KernelMode::kLockstep;
   if (m == "wavefront") return KernelMode::kWavefront;
   return KernelMode::kLean;
@@ -2515,16 +2576,18 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
   // Long renders are split into launches of at most `chunk` samples per
   // pixel; the running mean lives in the frame, so the result is identical.
-  const uint32_t chunk = 32;
+  const uint32_t chunk = kChunk;
   // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
   // produces identical frames): "lean" (default) path-regeneration megakernel
-  // with the unwind scratch in HBM rows and while-while traversal;
+  // with the unwind scratch in HBM rows, while-while traversal and the wave's
+  // (pixel, sample) tasks pooled across lanes; "lean_nopool" one pixel per lane;
   // "lean_bvh4" with 4-wide nodes for scenes uploaded with FS_BVH4=1 (slower:
   // more VALU per step); "lean_ifif" the single-loop traversal; "regen" with the unwind
   // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
   // extend/shade kernels over a compacted path queue.
   const KernelMode mode = kernel_mode();
-  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanBvh4 && mode != KernelMode::kLeanIfIf)
+  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanNoPool && mode != KernelMode::kLeanBvh4 &&
+      mode != KernelMode::kLeanIfIf)
     return fail(FS_ERR_INVALID, "textured scenes need the default (lean) kernel schedule");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
   if (mode == KernelMode::kWavefront && blocks && params->spp) {
@@ -2580,7 +2643,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     return FS_OK;
   }
   dev::WfState lean{};
-  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanBvh4 || mode == KernelMode::kLeanIfIf;
+  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanNoPool || mode == KernelMode::kLeanBvh4 ||
+                         mode == KernelMode::kLeanIfIf;
   if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
     if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean, ctx->has_textures))) return rc;
   }
@@ -2590,16 +2654,20 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     auto kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
     if (mode == KernelMode::kLockstep) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
     if (lean_mode) {
-      auto lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
+      // default: while-while BVH2 traversal, pooled (pixel, sample) tasks
+      auto lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true>
+                      : dev::render_kernel_lean<false, 6, true, false, false, true>;
       if (ctx->has_textures)  // textured scenes: the instantiation with texcoords + texel rows
-        lk = count ? dev::render_kernel_lean<true, 6, true, false, true>
-                   : dev::render_kernel_lean<false, 6, true, false, true>;
+        lk = count ? dev::render_kernel_lean<true, 6, true, false, true, true>
+                   : dev::render_kernel_lean<false, 6, true, false, true, true>;
+      else if (mode == KernelMode::kLeanNoPool)
+        lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
       else if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
       else if (mode == KernelMode::kLeanIfIf)
         lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
       hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
-                         lean.p0, lean.ovf, lean.tex, (DevCounters*)ctx->counters.p);
+                         lean.p0, lean.ovf, lean.tex, lean.rad, (DevCounters*)ctx->counters.p);
     } else {
       hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
                          (DevCounters*)ctx->counters.p);

@@ -14,6 +14,7 @@
 namespace fs {
 
 constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS columns
+constexpr uint32_t kChunk = 32;  // samples per pixel per launch (fs_render splits longer renders)
 
 struct DevScene {
   const DevObject* __restrict__ objects;
