@@ -982,6 +982,14 @@ __device__ __forceinline__ void wf_store_ray(const WfState& W, uint32_t slot, co
   W.ray2[slot] = r.stop.z;
 }
 
+// Object records are wave-uniform and never written by a kernel: reading
+// them through the constant address space lets the backend use scalar loads
+// (SGPRs) instead of vector loads of uniform data (VGPRs).
+typedef const __attribute__((address_space(4))) DevObject* ConstObj;
+__device__ __forceinline__ ConstObj const_obj(const DevObject* base, uint32_t i) {
+  return (ConstObj)(base) + i;
+}
+
 struct MinHit {
   float t, u, v;
   int32_t obj;
@@ -1286,7 +1294,8 @@ __device__ __forceinline__ void traverse4_ww(const DevScene& S, uint32_t root, i
 // test): the slab interval uses v_rcp and the same t margins as the BVH
 // traversal, against a box padded on the host (fs_scene.cpp). A segment that
 // can produce a hit with t < best always passes.
-__device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, const float* __restrict__ b) {
+template <class FloatPtr>
+__device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, FloatPtr b) {
   const float tiny = 1e-20f;
   float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
   float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
@@ -1321,10 +1330,11 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   h.point = 0;
   h.tc = -1;
   bool zl = zero_len(r);
-  for (uint32_t oi = 0; oi < S.num_objects; ++oi) {
-    const DevObject* __restrict__ o = S.objects + oi;
+  for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
+    const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
+    ConstObj o = const_obj(S.objects, oi);
     int32_t kind = o->kind;
-    const float* d = o->d;
+    const __attribute__((address_space(4))) float* d = o->d;
     if (kind == FS_OBJ_MESH) {
       if (!o->i2) continue;
       uint64_t t0 = FS_TICK();

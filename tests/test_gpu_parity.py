@@ -180,6 +180,17 @@ def test_empty_scene_is_all_sky(gpu_renderer):
         np.float32([0.75, 1.5, 3.0]), (16, 16, 3)))
 
 
+@pytest.mark.parametrize("dims", [(37, 29, 5), (9, 70, 3), (130, 7, 2)])
+def test_odd_frame_sizes(dims, scene_dir, gpu_renderer):
+    """Partial 8x8 micro-tiles and partial 64x64 tiles: the pooled schedule
+    enumerates only in-frame pixels; every plane must match the oracle."""
+    W, H, spp = dims
+    s = load_scene("c2", scene_dir)
+    out = gpu_render(gpu_renderer, s, s.camera(0), W, H, spp)
+    ref = oracle_render(s.desc_ptr(), s.camera(0), W, H, spp)
+    assert_parity(out, ref, exact=True)
+
+
 # ---- textures (material.cpp:108-126, object.cpp texcoords, mesh.cpp:300-311) -
 def textured_scene(spheres):
     """Textured Diffuse/Metal/Ceramic/Glow/Light on planar-mapped objects and
