@@ -1090,9 +1090,10 @@ __device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, i
 // parked leaves together. Inner-node and triangle code no longer interleave
 // per iteration. The closest hit is a total order on (t, face), so the test
 // order does not change the result.
-template <bool COUNT>
-__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl, MinHit& h,
+template <bool COUNT, int ZLMODE = -1>  // ZLMODE: 0/1 = ray known (non-)zero-length, -1 = runtime zl
+__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl_rt, MinHit& h,
                                           Tally<COUNT>& tally) {
+  const bool zl = ZLMODE < 0 ? zl_rt : ZLMODE == 1;
   uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
   for (uint32_t i = 0; i < cnt; i++) {
     uint32_t ti = first + i;
@@ -1129,16 +1130,19 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
   float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
   float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
   float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
-  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+  // v_rcp (about 1 ulp) instead of IEEE division: the slab test is a
+  // conservative cull whose t margins (1e-6 absolute, 2e-6 relative) and
+  // box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
+  float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
   float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
   uint32_t w = root, leaf = 0, sp = 0;
+  float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;  // h.t only changes in the leaf tests
   while (w != kNone || leaf) {
     while (!(w & kLeafBit) && w != kNone) {
       const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
       float4 X = q[0], Y = q[1], Z = q[2];
       uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       if (COUNT) tally.nodes++;
-      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
       bool h0, h1;
       float t0, t1;
       if (!zl) {
@@ -1186,6 +1190,7 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
         w = sp ? stk[--sp * kBlock] : kNone;
       }
     }
+    tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
   }
 }
 
@@ -2078,6 +2083,33 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   }
 }
 
+// TraceRange (engine.cpp:298-329): one query per lane, the camera ray through
+// (x, y) without jitter or aperture, Scene::Trace, distance to the hit point.
+__global__ __launch_bounds__(kBlock) void trace_range_kernel(DevScene S, DevCamera C, const float2* __restrict__ xy,
+                                                             uint32_t n, float* __restrict__ out) {
+  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float2 q = xy[i];
+  // engine.cpp:314-320: the jitter-free form of camera_ray's projection
+  float xd = (float)((double)C.hpw * ((double)(q.x / (C.width - 1)) * 2.0 - 1.0));
+  float yd = (float)((double)C.hph * ((double)(q.y / (C.height - 1)) * 2.0 - 1.0));
+  Ray r;
+  r.start = C.origin;
+  r.stop = C.proj_origin + C.right * xd + C.up * yd;
+  r.dir = r.stop - r.start;
+  MinHit h;
+  Tally<false> tally;
+  PhaseAcc pa;
+  scene_trace_min<false, true>(S, r, h, stk_all + threadIdx.x, tally, pa);
+  float d = C.z_far;
+  if (h.obj >= 0) {
+    f3 p = h.point ? r.start : r.start + r.dir * h.t;
+    d = length(p - C.origin);
+  }
+  out[i] = d;
+}
+
 // ---- multi-GPU packing: 10 words per pixel (colour, count, normal, depth, id)
 constexpr uint32_t kPackWords = 10;
 
@@ -2186,7 +2218,7 @@ struct fs_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
   DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send,
-      pack_recv;
+      pack_recv, range_io;
   bool has_textures = false;
   DevScene scene{};
   uint32_t num_objects = 0;
@@ -2411,7 +2443,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
-                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table,
+                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
     b->release();
   ctx->wf.release();
@@ -2640,7 +2672,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       FS_HIP(hipGetLastError());
       if ((rc = read_count(0, &live))) return rc;
     }
-    for (uint32_t it = 1; live; it++) {
+    while (live) {
       uint32_t g = (live + kBlock - 1) / kBlock;
       FS_HIP(hipMemsetAsync(W.count + (cur ^ 1u), 0, 4, ctx->stream));
       hipLaunchKernelGGL(ext, dim3(g), dim3(kBlock), 0, ctx->stream, ctx->scene, W, cur, 0u, L.spp, dc);
@@ -2725,6 +2757,28 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                c.phase[0], c.phase[1], c.phase[2], c.phase[5], c.phase[6], c.phase[7], c.phase[3], c.phase[4],
                c.phase[8], c.phase[9]);
 #endif
+  return FS_OK;
+}
+
+int fs_trace_range(fs_context* ctx, const fs_camera* camera, uint32_t width, uint32_t height, const float* xy,
+                   uint32_t count, float* distances) {
+  if (!ctx || !camera || (count && (!xy || !distances))) return fail(FS_ERR_INVALID, "null argument");
+  if (!ctx->have_scene) return fail(FS_ERR_STATE, "fs_trace_range before fs_upload_scene");
+  if (width < 2 || height < 2) return fail(FS_ERR_INVALID, "frame must be at least 2x2 (engine.cpp:300-303)");
+  if (!count) return FS_OK;
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  size_t in_bytes = 8ull * count, bytes = in_bytes + 4ull * count;
+  if ((rc = ensure(&ctx->range_io, bytes))) return rc;
+  float2* d_xy = (float2*)ctx->range_io.p;
+  float* d_out = (float*)((char*)ctx->range_io.p + in_bytes);
+  FS_HIP(hipMemcpyAsync(d_xy, xy, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+  DevCamera C = camera_basis(camera, width, height);
+  hipLaunchKernelGGL(dev::trace_range_kernel, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream,
+                     ctx->scene, C, d_xy, count, d_out);
+  FS_HIP(hipGetLastError());
+  FS_HIP(hipMemcpyAsync(distances, d_out, 4ull * count, hipMemcpyDeviceToHost, ctx->stream));
+  FS_HIP(hipStreamSynchronize(ctx->stream));
   return FS_OK;
 }
 

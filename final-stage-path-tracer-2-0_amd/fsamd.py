@@ -111,6 +111,7 @@ GPU_SYMBOLS = {
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
     "fs_comm_destroy": ([_VP], C.c_int),
+    "fs_trace_range": ([_VP, C.POINTER(fs_camera), C.c_uint32, C.c_uint32, _VP, C.c_uint32, _VP], C.c_int),
 }
 HOST_SYMBOLS = {
     "fsh_last_error": ([], C.c_char_p),
@@ -376,6 +377,14 @@ class Renderer:
         c = fs_counters()
         _check(gpu_lib().fs_read_counters(self.ctx, C.byref(c)), "fs_read_counters")
         return {k: getattr(c, k) for k, _ in fs_counters._fields_}
+
+    def trace_range(self, cam, width, height, xy):
+        """TraceRange (engine.cpp:298-329) for an (n, 2) array of image points."""
+        pts = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+        out = np.empty(len(pts), np.float32)
+        _check(gpu_lib().fs_trace_range(self.ctx, C.byref(cam), width, height, pts.ctypes.data, len(pts),
+                                        out.ctypes.data), "fs_trace_range")
+        return out
 
     # -- RCCL
     @staticmethod

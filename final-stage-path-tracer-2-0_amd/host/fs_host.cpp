@@ -798,6 +798,32 @@ const uint32* DisplayFrame::GetCountBuffer() {
 // ============================================================================
 // TraceScene — engine.cpp:253-296
 // ============================================================================
+namespace {
+// Uploads `scene` when it (or the normal table) changed since the last trace.
+bool ensure_scene(Engine& e, Scene* scene) {
+  if (ensure_context(e)) return false;
+  if (e.scene != scene || e.scene_version != scene->version() || e.table_version != g_table_version) {
+    std::string err;
+    const fs_scene_desc* d = scene->Describe(&err);
+    if (!d) {
+      e.status = FS_ERR_INVALID;
+      e.error = err;
+      std::fprintf(stderr, "[fs] %s\n", err.c_str());
+      return false;
+    }
+    int rc = fs_upload_scene(e.ctx, d);
+    if (rc) {
+      engine_fail(e, rc, "fs_upload_scene");
+      return false;
+    }
+    e.scene = scene;
+    e.scene_version = scene->version();
+    e.table_version = g_table_version;
+  }
+  return true;
+}
+}  // namespace
+
 void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uint32 spp) {
   Engine& e = engine();
   std::lock_guard<std::mutex> g(e.mu);
@@ -808,25 +834,7 @@ void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uin
     e.error = "TraceScene: null scene or frame";
     return;
   }
-  if (ensure_context(e)) return;
-  if (e.scene != scene || e.scene_version != scene->version() || e.table_version != g_table_version) {
-    std::string err;
-    const fs_scene_desc* d = scene->Describe(&err);
-    if (!d) {
-      e.status = FS_ERR_INVALID;
-      e.error = err;
-      std::fprintf(stderr, "[fs] %s\n", err.c_str());
-      return;
-    }
-    int rc = fs_upload_scene(e.ctx, d);
-    if (rc) {
-      engine_fail(e, rc, "fs_upload_scene");
-      return;
-    }
-    e.scene = scene;
-    e.scene_version = scene->version();
-    e.table_version = g_table_version;
-  }
+  if (!ensure_scene(e, scene)) return;
   fs_camera cam = view.Describe();
   fs_render_params p;
   std::memset(&p, 0, sizeof(p));
@@ -852,6 +860,24 @@ void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uin
 
 void TraceScene(const Camera& view, Scene* scene, DisplayFrame* output, ImagePlaneCache*) {
   TraceSceneBatch(view, scene, output, 1);
+}
+
+float32 TraceRange(const Camera& view, Scene* scene, DisplayFrame* frame, float32 x, float32 y) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  e.status = FS_OK;
+  e.error.clear();
+  if (!scene || !frame) {
+    e.status = FS_ERR_INVALID;
+    e.error = "TraceRange: null scene or frame";
+    return view.z_far;
+  }
+  if (!ensure_scene(e, scene)) return view.z_far;
+  fs_camera cam = view.Describe();
+  float xy[2] = {x, y}, d = view.z_far;
+  int rc = fs_trace_range(e.ctx, &cam, frame->GetWidth(), frame->GetHeight(), xy, 1, &d);
+  if (rc) engine_fail(e, rc, "fs_trace_range");
+  return d;
 }
 
 }  // namespace base

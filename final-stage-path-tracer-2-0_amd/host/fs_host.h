@@ -373,6 +373,9 @@ class ImagePlaneCache;  // accepted and ignored, as main.cpp:157 never passes on
 void TraceScene(const Camera& view, Scene* scene, DisplayFrame* output, ImagePlaneCache* cache = nullptr);
 // Adds `spp` samples per pixel in one device submission (== spp TraceScene calls).
 void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uint32 spp);
+// engine.cpp:298-329: distance from view.origin to the first hit of the
+// jitter-free ray through frame point (x, y), or view.z_far (focus picking).
+float32 TraceRange(const Camera& view, Scene* scene, DisplayFrame* frame, float32 x, float32 y);
 // Device used by TraceScene (default 0); must be called before the first trace.
 bool SetTraceDevice(int device);
 // fs_status of the last engine call and its message.

@@ -250,6 +250,15 @@ int fs_frame_gather(fs_context* ctx, fs_frame* frame,
                     const fs_render_params* params, int root);
 int fs_comm_destroy(fs_context* ctx);
 
+/* ---- TraceRange (engine.cpp:298-329) ------------------------------------
+ * Focus pick: for each of `count` image points (x, y interleaved in xy) of a
+ * width x height frame, the distance from camera->origin to the first hit of
+ * the jitter-free, aperture-free camera ray through that point, or
+ * camera->z_far when nothing is hit. Synchronous; xy and distances are host
+ * memory. */
+int fs_trace_range(fs_context* ctx, const fs_camera* camera, uint32_t width, uint32_t height,
+                   const float* xy, uint32_t count, float* distances);
+
 #ifdef __cplusplus
 }
 #endif

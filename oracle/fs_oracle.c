@@ -1283,6 +1283,26 @@ int oracle_trace_sample(const oracle_scene* sc, const fs_camera* cam, uint32_t W
   return 0;
 }
 
+/* TraceRange (engine.cpp:298-329): the jitter-free ray through (x, y). */
+int oracle_trace_range(const oracle_scene* sc, const fs_camera* cam, uint32_t W, uint32_t H, float x, float y,
+                       float* distance) {
+  if (!sc || !cam || !distance || W < 2 || H < 2) return FS_ERR_INVALID;
+  cambasis b;
+  camera_basis(cam, W, H, &b);
+  float xd = (float)((double)b.hpw * ((double)(x / (b.width - 1)) * 2.0 - 1.0));
+  float yd = (float)((double)b.hph * ((double)(y / (b.height - 1)) * 2.0 - 1.0));
+  v3 origin = mk3(cam->origin[0], cam->origin[1], cam->origin[2]);
+  v3 stop = add3(add3(b.proj_origin, scl3(b.right, xd)), scl3(b.up, yd));
+  ray_t r = mkray(origin, stop);
+  ocoll ci;
+  if (!scene_trace(sc, &r, &ci, NULL)) {
+    *distance = cam->z_far;
+    return 0;
+  }
+  *distance = len3(sub3(ci.point, origin));
+  return 0;
+}
+
 /* ---- KAT wrappers ---- */
 float oracle_inv_sqrt(float f) { return inv_sqrt_ref(f); }
 float oracle_fast_sqrt(float f) { return fsqrt(f); }

@@ -66,6 +66,12 @@ int oracle_trace_sample(const oracle_scene* scene, const fs_camera* camera,
                         float normal[3], float* depth, uint64_t* material_id,
                         uint32_t* ray_count);
 
+/* TraceRange (engine.cpp:298-329): distance to the first hit of the
+ * jitter-free ray through image point (x, y), or camera->z_far. */
+int oracle_trace_range(const oracle_scene* scene, const fs_camera* camera,
+                       uint32_t width, uint32_t height, float x, float y,
+                       float* distance);
+
 /* ---- known-answer helpers ---------------------------------------------- */
 uint64_t oracle_splitmix64(uint64_t x);
 uint64_t oracle_pixel_seed(uint64_t pixel, uint64_t sample, uint64_t seed);

@@ -39,6 +39,7 @@ def lib():
         L.oracle_trace_sample.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_uint32, C.c_uint32, C.c_uint64, F, F, F,
                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        L.oracle_trace_range.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_float, C.c_float, F]
         L.oracle_splitmix64.restype = C.c_uint64
         L.oracle_splitmix64.argtypes = [C.c_uint64]
         L.oracle_pixel_seed.restype = C.c_uint64
@@ -138,6 +139,16 @@ class Scene:
         lib().oracle_trace_sample(self.h, C.byref(cam), width, height, x, y, sample, seed, col, nrm,
                                   C.byref(dep), C.byref(mid), C.byref(rc_))
         return np.array(col[:], np.float32), np.array(nrm[:], np.float32), dep.value, mid.value, rc_.value
+
+    def trace_range(self, cam, width, height, xy):
+        out = []
+        for x, y in np.asarray(xy, np.float32).reshape(-1, 2):
+            d = C.c_float()
+            rc = lib().oracle_trace_range(self.h, C.byref(cam), width, height, C.c_float(x), C.c_float(y), C.byref(d))
+            if rc:
+                raise RuntimeError(f"oracle_trace_range failed ({rc})")
+            out.append(d.value)
+        return np.array(out, np.float32)
 
     def mesh_info(self, m):
         n = C.c_uint32()

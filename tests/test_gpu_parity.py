@@ -191,6 +191,23 @@ def test_odd_frame_sizes(dims, scene_dir, gpu_renderer):
     assert_parity(out, ref, exact=True)
 
 
+def test_trace_range_matches_oracle(scene_dir, gpu_renderer):
+    """TraceRange (engine.cpp:298-329): focus-pick distances, hits and misses."""
+    rng = np.random.default_rng(5)
+    for name, W, H in (("c2", 640, 360), ("c4", 1920, 1080)):
+        s = load_scene(name, scene_dir)
+        cam = s.camera(0)
+        xy = np.concatenate([rng.random((200, 2)) * [W - 1, H - 1],
+                             [[0, 0], [W - 1, H - 1], [W / 2, H / 2], [-50, 10], [W + 400, H + 400]]]).astype(np.float32)
+        gpu_renderer.upload(s)
+        got = gpu_renderer.trace_range(cam, W, H, xy)
+        o = oracle_py.Scene(s.desc_ptr())
+        ref = o.trace_range(cam, W, H, xy)
+        o.close()
+        np.testing.assert_array_equal(got, ref)
+        assert (got < cam.z_far).any() and (got == np.float32(cam.z_far)).any()
+
+
 # ---- textures (material.cpp:108-126, object.cpp texcoords, mesh.cpp:300-311) -
 def textured_scene(spheres):
     """Textured Diffuse/Metal/Ceramic/Glow/Light on planar-mapped objects and
