@@ -2760,6 +2760,31 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   return FS_OK;
 }
 
+int fs_prepare_digest(const fs_scene_desc* desc, uint64_t* digest, uint64_t* num_nodes, double* build_ms) {
+  if (!desc || !digest) return fail(FS_ERR_INVALID, "null argument");
+  std::string err;
+  PreparedScene P;
+  int rc = prepare_scene(desc, &P, &err);
+  if (rc) return fail(rc, err);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over every uploaded array
+  auto mix = [&h](const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  mix(P.objects.data(), P.objects.size() * sizeof(DevObject));
+  mix(P.nodes.data(), P.nodes.size() * sizeof(BvhNode));
+  mix(P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node));
+  mix(P.tris.data(), P.tris.size() * sizeof(DevTri));
+  mix(P.tri_normals.data(), P.tri_normals.size() * sizeof(float));
+  mix(P.tri_tex.data(), P.tri_tex.size() * sizeof(float));
+  mix(P.materials.data(), P.materials.size() * sizeof(fs_material));
+  mix(P.tex_rgb.data(), P.tex_rgb.size() * sizeof(float));
+  *digest = h;
+  if (num_nodes) *num_nodes = P.nodes.size();
+  if (build_ms) *build_ms = P.build_ms;
+  return FS_OK;
+}
+
 int fs_trace_range(fs_context* ctx, const fs_camera* camera, uint32_t width, uint32_t height, const float* xy,
                    uint32_t count, float* distances) {
   if (!ctx || !camera || (count && (!xy || !distances))) return fail(FS_ERR_INVALID, "null argument");

@@ -14,8 +14,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <cstring>
+#include <memory>
 
 namespace fs {
 namespace {
@@ -158,6 +161,16 @@ constexpr int kBins = 16;
 uint32_t leaf_target_env() {
   uint32_t v = std::getenv("FS_BVH_LEAF") ? (uint32_t)std::atoi(std::getenv("FS_BVH_LEAF")) : 2u;
   return (v && v <= kMaxLeafCount) ? v : 2u;
+}
+
+// Subtrees are built concurrently down to this depth (2^depth threads);
+// FS_BVH_THREADS=1 builds sequentially (same tree, same layout).
+uint32_t parallel_depth_env() {
+  const char* e = std::getenv("FS_BVH_THREADS");
+  if (!e) return 4;
+  int t = std::atoi(e), d = 0;
+  while (d < 8 && (1 << (d + 1)) <= t) d++;
+  return (uint32_t)d;
 }
 
 class BvhBuilder {
@@ -314,10 +327,68 @@ class BvhBuilder {
     return m;
   }
   // Builds the two children of `node` over [b,e).
+  // A subtree built into its own arrays (node and triangle indices local),
+  // merged into the parent builder afterwards.
+  struct Local {
+    std::vector<BvhNode> nodes;
+    std::vector<DevTri> tris;
+    std::vector<float> normals, tex;
+    std::unique_ptr<BvhBuilder> b;
+  };
+  void init_local(Local* L) const {
+    L->b.reset(new BvhBuilder(&L->nodes, &L->tris, &L->normals, &L->tex, mesh_tris_, mesh_normals_, mesh_tex_));
+    L->b->prims_ = prims_;
+    L->b->leaf_ = leaf_;
+    L->b->par_depth_ = par_depth_;
+  }
+  // Appends a local subtree after everything built so far: the result is the
+  // same DFS layout the sequential build produces. Returns the subtree root.
+  uint32_t merge(Local& L) {
+    const uint32_t node_off = (uint32_t)nodes_->size(), tri_off = (uint32_t)tris_->size();
+    for (BvhNode n : L.nodes) {
+      for (int c = 0; c < 2; c++) {
+        uint32_t w = n.child[c];
+        if (!(w & kLeafBit))
+          n.child[c] = w + node_off;
+        else if ((w >> 24) & 0x7Fu)
+          n.child[c] = (w & ~0xFFFFFFu) | ((w & 0xFFFFFFu) + tri_off);
+      }
+      nodes_->push_back(n);
+    }
+    tris_->insert(tris_->end(), L.tris.begin(), L.tris.end());
+    tri_normals_->insert(tri_normals_->end(), L.normals.begin(), L.normals.end());
+    tri_tex_->insert(tri_tex_->end(), L.tex.begin(), L.tex.end());
+    max_depth_ = std::max(max_depth_, L.b->max_depth_);
+    overflow_ = overflow_ || L.b->overflow_;
+    return node_off;
+  }
+
+  static constexpr uint32_t kParallelMin = 1u << 14;  // primitives below which a subtree stays on its thread
+
   void split_into(uint32_t node, uint32_t b, uint32_t e, uint32_t depth) {
     max_depth_ = std::max(max_depth_, depth);
     uint32_t m = partition(b, e, depth);
     uint32_t ranges[2][2] = {{b, m}, {m, e}};
+    const bool leaf0 = m - b <= leaf_ || depth + 1 >= kTraversalStack - 1;
+    const bool leaf1 = e - m <= leaf_ || depth + 1 >= kTraversalStack - 1;
+    if (e - b >= kParallelMin && depth < par_depth_ && !leaf0 && !leaf1) {
+      // Both children are subtrees: build them concurrently (disjoint prim
+      // ranges), then append them in child order.
+      Box boxes[2] = {range_box(b, m), range_box(m, e)};
+      Local L0, L1;
+      init_local(&L0);
+      init_local(&L1);
+      auto job = [depth](Local* L, uint32_t cb, uint32_t ce) {
+        uint32_t r = L->b->alloc_node();
+        L->b->split_into(r, cb, ce, depth + 1);
+      };
+      std::thread t(job, &L1, m, e);
+      job(&L0, b, m);
+      t.join();
+      set_child(node, 0, boxes[0], merge(L0));
+      set_child(node, 1, boxes[1], merge(L1));
+      return;
+    }
     for (int s = 0; s < 2; s++) {
       uint32_t cb = ranges[s][0], ce = ranges[s][1];
       Box cbox = range_box(cb, ce);
@@ -340,6 +411,7 @@ class BvhBuilder {
   const std::vector<float>* mesh_tex_;
   std::vector<Prim>* prims_ = nullptr;
   uint32_t leaf_ = leaf_target_env();
+  uint32_t par_depth_ = parallel_depth_env();
   uint32_t max_depth_ = 0;
   bool overflow_ = false;
 };
@@ -723,6 +795,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       *err = "too many triangles for the 24-bit leaf encoding";
       return FS_ERR_INVALID;
     }
+    auto tp = std::chrono::steady_clock::now();
     std::vector<Prim> prims(m.num_triangles);
     for (uint32_t f = 0; f < m.num_triangles; f++) {
       Prim& p = prims[f];
@@ -734,7 +807,13 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     }
     for (DevTri& t : mtris) t.mesh_obj = mi;
     BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex);
+    auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
+    if (std::getenv("FS_BUILD_LOG"))
+      std::fprintf(stderr, "[fs build] mesh %u: %u tris, prepare %.1f ms, prims %.1f ms, bvh %.1f ms\n", mi,
+                   m.num_triangles, std::chrono::duration<double, std::milli>(tp - t0).count(),
+                   std::chrono::duration<double, std::milli>(tb - tp).count(),
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
     if (mesh_out[mi].root == 0xFFFFFFFFu) {
       *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
       return FS_ERR_INVALID;

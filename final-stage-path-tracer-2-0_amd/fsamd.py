@@ -111,6 +111,7 @@ GPU_SYMBOLS = {
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
     "fs_comm_destroy": ([_VP], C.c_int),
+    "fs_prepare_digest": ([_VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double)], C.c_int),
     "fs_trace_range": ([_VP, C.POINTER(fs_camera), C.c_uint32, C.c_uint32, _VP, C.c_uint32, _VP], C.c_int),
 }
 HOST_SYMBOLS = {
@@ -431,3 +432,10 @@ def load_exr(path):
         return np.ctypeslib.as_array(buf, shape=(h.value * w.value * 4,)).reshape(h.value, w.value, 4).copy()
     finally:
         lib.fsh_free(buf)
+
+
+def prepare_digest(desc_ptr):
+    """fs_prepare_digest: host-only scene preparation; (digest, nodes, build_ms)."""
+    d, n, ms = C.c_uint64(), C.c_uint64(), C.c_double()
+    _check(gpu_lib().fs_prepare_digest(desc_ptr, C.byref(d), C.byref(n), C.byref(ms)), "fs_prepare_digest")
+    return d.value, n.value, ms.value

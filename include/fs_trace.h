@@ -250,6 +250,12 @@ int fs_frame_gather(fs_context* ctx, fs_frame* frame,
                     const fs_render_params* params, int root);
 int fs_comm_destroy(fs_context* ctx);
 
+/* Host only (no device needed): runs the scene preparation of
+ * fs_upload_scene (object constructors, BVH build) and returns a 64-bit
+ * digest of every array it would upload, the BVH node count and the build
+ * time. For build reproducibility checks and load-time measurements. */
+int fs_prepare_digest(const fs_scene_desc* desc, uint64_t* digest, uint64_t* num_nodes, double* build_ms);
+
 /* ---- TraceRange (engine.cpp:298-329) ------------------------------------
  * Focus pick: for each of `count` image points (x, y interleaved in xy) of a
  * width x height frame, the distance from camera->origin to the first hit of

@@ -187,3 +187,19 @@ def test_generated_scene_sizes(scene_dir):
     assert f.shape == (10000, 3) and v.shape == (51 * 100, 3)
     path, ntri = scenes.write_c3(os.path.join(scene_dir, "c3_count"))
     assert abs(ntri - 250_000) / 250_000 < 0.01
+
+
+def test_parallel_bvh_build_is_reproducible(scene_dir, monkeypatch):
+    """The BVH build runs subtrees on threads; the uploaded arrays (nodes,
+    triangles, normals, objects) must be byte-identical to the sequential
+    build (fs_prepare_digest, host only)."""
+    import fsamd
+    from conftest import load_scene
+
+    s = load_scene("c3", scene_dir)
+    digests = set()
+    for threads in ("1", "2", "16"):
+        monkeypatch.setenv("FS_BVH_THREADS", threads)
+        d, nodes, ms = fsamd.prepare_digest(s.desc_ptr())
+        digests.add((d, nodes))
+    assert len(digests) == 1
