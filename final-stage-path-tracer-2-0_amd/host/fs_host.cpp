@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <limits>
 #include <mutex>
 #include <sstream>
 
@@ -324,93 +325,283 @@ fs_object QuadObject::Describe() const {
 }
 
 // ---- Wavefront OBJ ----------------------------------------------------------
-static bool parse_corner(const char* tok, int32 nv, int32 nt, int32 nn, int32* v, int32* t, int32* n) {
-  // v, v/t, v//n, v/t/n; negative = relative (tinyobj fixIndex)
-  auto fix = [](long idx, int32 count) -> int32 {
-    if (idx > 0) return (int32)(idx - 1);
-    if (idx < 0) return (int32)(count + idx);
-    return -1;
-  };
-  char* end;
-  long a = std::strtol(tok, &end, 10);
-  *v = fix(a, nv);
-  *t = -1;
-  *n = -1;
-  if (*end == '/') {
-    const char* p = end + 1;
-    if (*p != '/') {
-      long b = std::strtol(p, &end, 10);
-      *t = fix(b, nt);
-      p = end;
+// Restates the parts of the vendored tinyobj loader (tiny_obj_loader.h) that
+// decide the triangles MeshObject sees: its number parser, index fixing and
+// the ear-clipping triangulation of polygons.
+namespace {
+
+// tryParseDouble (tiny_obj_loader.h:537-650): digits accumulated in double,
+// fraction digits as digit * 10^-k, exponent applied as ldexp(m * 5^e, e).
+bool try_parse_double(const char* s, const char* s_end, double* result) {
+  if (s >= s_end) return false;
+  double mantissa = 0.0;
+  int exponent = 0;
+  char sign = '+', exp_sign = '+';
+  const char* curr = s;
+  int read = 0;
+  bool end_not_reached = false;
+  auto is_digit = [](char c) { return c >= '0' && c <= '9'; };
+  if (*curr == '+' || *curr == '-') {
+    sign = *curr;
+    curr++;
+  } else if (!is_digit(*curr)) {
+    return false;
+  }
+  end_not_reached = curr != s_end;
+  while (end_not_reached && is_digit(*curr)) {
+    mantissa *= 10;
+    mantissa += (int)(*curr - 0x30);
+    curr++;
+    read++;
+    end_not_reached = curr != s_end;
+  }
+  if (read == 0) return false;
+  if (end_not_reached) {
+    bool parse_exp = false;
+    if (*curr == '.') {
+      curr++;
+      read = 1;
+      end_not_reached = curr != s_end;
+      static const double pow_lut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+      while (end_not_reached && is_digit(*curr)) {
+        mantissa += (int)(*curr - 0x30) * (read < 8 ? pow_lut[read] : std::pow(10.0, -read));
+        read++;
+        curr++;
+        end_not_reached = curr != s_end;
+      }
+      parse_exp = end_not_reached;
+    } else if (*curr == 'e' || *curr == 'E') {
+      parse_exp = true;
     }
-    if (*p == '/') {
-      long c = std::strtol(p + 1, &end, 10);
-      *n = fix(c, nn);
+    if (parse_exp && (*curr == 'e' || *curr == 'E')) {
+      curr++;
+      end_not_reached = curr != s_end;
+      if (end_not_reached && (*curr == '+' || *curr == '-')) {
+        exp_sign = *curr;
+        curr++;
+      } else if (!is_digit(*curr)) {
+        return false;
+      }
+      read = 0;
+      end_not_reached = curr != s_end;
+      while (end_not_reached && is_digit(*curr)) {
+        exponent *= 10;
+        exponent += (int)(*curr - 0x30);
+        curr++;
+        read++;
+        end_not_reached = curr != s_end;
+      }
+      exponent *= (exp_sign == '+' ? 1 : -1);
+      if (read == 0) return false;
     }
   }
-  return *v >= 0;
+  *result = (sign == '+' ? 1 : -1) * (exponent ? std::ldexp(mantissa * std::pow(5.0, exponent), exponent) : mantissa);
+  return true;
 }
 
+// parseReal (tiny_obj_loader.h:652-660): the token ends at space, tab or CR.
+float32 parse_real(const char** token, double default_value = 0.0) {
+  (*token) += std::strspn(*token, " \t");
+  const char* end = (*token) + std::strcspn(*token, " \t\r\n");
+  double val = default_value;
+  try_parse_double(*token, end, &val);
+  *token = end;
+  return (float32)val;
+}
+
+// fixIndex (tiny_obj_loader.h:471-492): 1-based, negative = relative.
+bool fix_index(int idx, int n, int* ret) {
+  if (idx > 0) {
+    *ret = idx - 1;
+    return true;
+  }
+  if (idx == 0) return false;
+  *ret = n + idx;
+  return true;
+}
+
+struct Corner {
+  int v = -1, t = -1, n = -1;
+};
+
+// parseTriple (v, v/vt, v//vn, v/vt/vn).
+bool parse_corner(const char** token, int nv, int nn, int nt, Corner* c) {
+  const char* p = *token;
+  if (!fix_index(std::atoi(p), nv, &c->v)) return false;
+  p += std::strcspn(p, "/ \t\r\n");
+  if (*p == '/') {
+    p++;
+    if (*p == '/') {  // v//vn
+      p++;
+      if (!fix_index(std::atoi(p), nn, &c->n)) return false;
+      p += std::strcspn(p, "/ \t\r\n");
+    } else {  // v/vt or v/vt/vn
+      if (!fix_index(std::atoi(p), nt, &c->t)) return false;
+      p += std::strcspn(p, "/ \t\r\n");
+      if (*p == '/') {
+        p++;
+        if (!fix_index(std::atoi(p), nn, &c->n)) return false;
+        p += std::strcspn(p, "/ \t\r\n");
+      }
+    }
+  }
+  *token = p;
+  return true;
+}
+
+// pnpoly (tiny_obj_loader.h:1019-1029)
+int pnpoly(int nvert, const float32* vertx, const float32* verty, float32 testx, float32 testy) {
+  int c = 0;
+  for (int i = 0, j = nvert - 1; i < nvert; j = i++) {
+    if (((verty[i] > testy) != (verty[j] > testy)) &&
+        (testx < (vertx[j] - vertx[i]) * (testy - verty[i]) / (verty[j] - verty[i]) + vertx[i]))
+      c = !c;
+  }
+  return c;
+}
+
+// exportGroupsToShape with triangulate = true (tiny_obj_loader.h:1042-1236):
+// ear clipping in the dominant plane of the first non-degenerate corner.
+void triangulate_face(const std::vector<float32>& v, const std::vector<Corner>& face, std::vector<Corner>* out) {
+  size_t npolys = face.size();
+  if (npolys < 3) return;
+  size_t axes[2] = {1, 2};
+  const float32 epsilon = std::numeric_limits<float32>::epsilon();
+  for (size_t k = 0; k < npolys; ++k) {
+    size_t vi0 = (size_t)face[(k + 0) % npolys].v, vi1 = (size_t)face[(k + 1) % npolys].v,
+           vi2 = (size_t)face[(k + 2) % npolys].v;
+    if (3 * vi0 + 2 >= v.size() || 3 * vi1 + 2 >= v.size() || 3 * vi2 + 2 >= v.size()) continue;
+    float32 e0x = v[vi1 * 3 + 0] - v[vi0 * 3 + 0], e0y = v[vi1 * 3 + 1] - v[vi0 * 3 + 1],
+            e0z = v[vi1 * 3 + 2] - v[vi0 * 3 + 2];
+    float32 e1x = v[vi2 * 3 + 0] - v[vi1 * 3 + 0], e1y = v[vi2 * 3 + 1] - v[vi1 * 3 + 1],
+            e1z = v[vi2 * 3 + 2] - v[vi1 * 3 + 2];
+    float32 cx = std::fabs(e0y * e1z - e0z * e1y);
+    float32 cy = std::fabs(e0z * e1x - e0x * e1z);
+    float32 cz = std::fabs(e0x * e1y - e0y * e1x);
+    if (cx > epsilon || cy > epsilon || cz > epsilon) {
+      if (!(cx > cy && cx > cz)) {
+        axes[0] = 0;
+        if (cz > cx && cz > cy) axes[1] = 1;
+      }
+      break;
+    }
+  }
+  float32 area = 0;
+  for (size_t k = 0; k < npolys; ++k) {
+    size_t vi0 = (size_t)face[(k + 0) % npolys].v, vi1 = (size_t)face[(k + 1) % npolys].v;
+    if (vi0 * 3 + axes[0] >= v.size() || vi0 * 3 + axes[1] >= v.size() || vi1 * 3 + axes[0] >= v.size() ||
+        vi1 * 3 + axes[1] >= v.size())
+      continue;
+    float32 v0x = v[vi0 * 3 + axes[0]], v0y = v[vi0 * 3 + axes[1]];
+    float32 v1x = v[vi1 * 3 + axes[0]], v1y = v[vi1 * 3 + axes[1]];
+    area += (v0x * v1y - v0y * v1x) * (float32)0.5;
+  }
+  int max_rounds = 10;
+  std::vector<Corner> rem = face;
+  size_t guess_vert = 0;
+  Corner ind[3];
+  float32 vx[3], vy[3];
+  while (rem.size() > 3 && max_rounds > 0) {
+    npolys = rem.size();
+    if (guess_vert >= npolys) {
+      max_rounds -= 1;
+      guess_vert -= npolys;
+    }
+    for (size_t k = 0; k < 3; k++) {
+      ind[k] = rem[(guess_vert + k) % npolys];
+      size_t vi = (size_t)ind[k].v;
+      if (vi * 3 + axes[0] >= v.size() || vi * 3 + axes[1] >= v.size()) {
+        vx[k] = 0.0f;
+        vy[k] = 0.0f;
+      } else {
+        vx[k] = v[vi * 3 + axes[0]];
+        vy[k] = v[vi * 3 + axes[1]];
+      }
+    }
+    float32 e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
+    float32 cross = e0x * e1y - e0y * e1x;
+    if (cross * area < (float32)0.0) {  // an internal (reflex) angle
+      guess_vert += 1;
+      continue;
+    }
+    bool overlap = false;
+    for (size_t other = 3; other < npolys; ++other) {
+      size_t idx = (guess_vert + other) % npolys;
+      size_t ovi = (size_t)rem[idx].v;
+      if (ovi * 3 + axes[0] >= v.size() || ovi * 3 + axes[1] >= v.size()) continue;
+      if (pnpoly(3, vx, vy, v[ovi * 3 + axes[0]], v[ovi * 3 + axes[1]])) {
+        overlap = true;
+        break;
+      }
+    }
+    if (overlap) {
+      guess_vert += 1;
+      continue;
+    }
+    out->push_back(ind[0]);  // an ear
+    out->push_back(ind[1]);
+    out->push_back(ind[2]);
+    size_t removed = (guess_vert + 1) % npolys;
+    while (removed + 1 < npolys) {
+      rem[removed] = rem[removed + 1];
+      removed += 1;
+    }
+    rem.pop_back();
+  }
+  if (rem.size() == 3) {
+    out->push_back(rem[0]);
+    out->push_back(rem[1]);
+    out->push_back(rem[2]);
+  }
+}
+
+}  // namespace
+
 bool LoadObjFile(const std::string& filename, MeshData* out, std::string* err) {
-  FILE* fp = std::fopen(filename.c_str(), "rb");
-  if (!fp) {
+  std::ifstream in(filename, std::ios::in | std::ios::binary);
+  if (!in) {
     *err = "cannot open " + filename;
     return false;
   }
   MeshData d;
-  std::vector<char> line(1 << 16);
-  std::vector<int32> cv, ct, cn;
-  while (std::fgets(line.data(), (int)line.size(), fp)) {
-    char* s = line.data();
-    while (*s == ' ' || *s == '\t') s++;
-    if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) {
-      char* e;
-      float32 x = std::strtof(s + 2, &e), y = std::strtof(e, &e), z = std::strtof(e, &e);
-      d.positions.push_back(x);
-      d.positions.push_back(y);
-      d.positions.push_back(z);
-    } else if (s[0] == 'v' && s[1] == 'n') {
-      char* e;
-      float32 x = std::strtof(s + 2, &e), y = std::strtof(e, &e), z = std::strtof(e, &e);
-      d.normals.push_back(x);
-      d.normals.push_back(y);
-      d.normals.push_back(z);
-    } else if (s[0] == 'v' && s[1] == 't') {
-      char* e;
-      float32 u = std::strtof(s + 2, &e), v = std::strtof(e, &e);
-      d.texcoords.push_back(u);
-      d.texcoords.push_back(v);
-    } else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
-      cv.clear();
-      ct.clear();
-      cn.clear();
-      char* p = s + 1;
-      int32 nv = (int32)(d.positions.size() / 3), nt = (int32)(d.texcoords.size() / 2),
-            nn = (int32)(d.normals.size() / 3);
-      while (*p) {
-        while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n') p++;
-        if (!*p) break;
-        int32 v, t, n;
-        if (!parse_corner(p, nv, nt, nn, &v, &t, &n)) break;
-        cv.push_back(v);
-        ct.push_back(t);
-        cn.push_back(n);
-        while (*p && *p != ' ' && *p != '\t' && *p != '\r' && *p != '\n') p++;
-      }
-      // Triangles pass through unchanged (tinyobj triangulation is the
-      // identity for them); larger polygons are fan-triangulated (parity of
-      // tinyobj's ear clipping is not pinned).
-      for (size_t k = 1; k + 1 < cv.size(); k++) {
-        size_t idx[3] = {0, k, k + 1};
-        for (size_t c : idx) {
-          d.corners.push_back(cv[c]);
-          d.corners.push_back(cn[c]);
-          d.corners.push_back(ct[c]);
+  std::string line;
+  std::vector<Corner> face, tris;
+  while (std::getline(in, line)) {
+    const char* token = line.c_str();
+    token += std::strspn(token, " \t");
+    if (token[0] == '\0' || token[0] == '#') continue;
+    auto is_space = [](char c) { return c == ' ' || c == '\t'; };
+    if (token[0] == 'v' && is_space(token[1])) {  // v x y z
+      token += 2;
+      float32 x = parse_real(&token), y = parse_real(&token), z = parse_real(&token);
+      d.positions.insert(d.positions.end(), {x, y, z});
+    } else if (token[0] == 'v' && token[1] == 'n' && is_space(token[2])) {
+      token += 3;
+      float32 x = parse_real(&token), y = parse_real(&token), z = parse_real(&token);
+      d.normals.insert(d.normals.end(), {x, y, z});
+    } else if (token[0] == 'v' && token[1] == 't' && is_space(token[2])) {
+      token += 3;
+      float32 u = parse_real(&token), v = parse_real(&token);
+      d.texcoords.insert(d.texcoords.end(), {u, v});
+    } else if (token[0] == 'f' && is_space(token[1])) {
+      token += 2;
+      token += std::strspn(token, " \t");
+      face.clear();
+      int nv = (int)(d.positions.size() / 3), nn = (int)(d.normals.size() / 3), nt = (int)(d.texcoords.size() / 2);
+      while (*token && *token != '\r' && *token != '\n') {
+        Corner c;
+        if (!parse_corner(&token, nv, nn, nt, &c)) {
+          *err = filename + ": failed to parse a face";
+          return false;
         }
+        face.push_back(c);
+        token += std::strspn(token, " \t\r");
       }
+      tris.clear();
+      triangulate_face(d.positions, face, &tris);
+      for (const Corner& c : tris) d.corners.insert(d.corners.end(), {c.v, c.n, c.t});
     }
   }
-  std::fclose(fp);
   *out = std::move(d);
   return true;
 }

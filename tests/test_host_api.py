@@ -203,3 +203,36 @@ def test_parallel_bvh_build_is_reproducible(scene_dir, monkeypatch):
         d, nodes, ms = fsamd.prepare_digest(s.desc_ptr())
         digests.add((d, nodes))
     assert len(digests) == 1
+
+
+def test_obj_numbers_follow_tinyobj_parser(tmp_path):
+    """tryParseDouble (tiny_obj_loader.h:537-650) is not correctly rounded: it
+    accumulates fraction digits in double before the float cast. These two
+    strings sit just above a float32 rounding midpoint; tinyobj (and the
+    mirror) round them down, a correctly rounded strtof rounds them up."""
+    import fsamd
+
+    p = tmp_path / "n.obj"
+    p.write_text("v 0.300000086426734924316406251 1.7000001072883605957031251 -2.5e-1\n"
+                 "v 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    pos, _ = fsamd.load_obj(str(p))
+    assert pos[0, 0] == np.float32(0.30000007152557373)
+    assert pos[0, 1] == np.float32(1.7000000476837158)
+    assert pos[0, 2] == np.float32(-0.25)
+
+
+def test_obj_polygons_ear_clipped_like_tinyobj(tmp_path):
+    """Polygon faces are triangulated by tinyobj's ear clipping
+    (tiny_obj_loader.h:1042-1236), not a fan: for this C-shaped octagon a fan
+    from vertex 0 would cross the notch. Expected ears worked by hand."""
+    import fsamd
+
+    p = tmp_path / "c.obj"
+    verts = [(0, 0), (3, 0), (3, 1), (1, 1), (1, 2), (3, 2), (3, 3), (0, 3)]
+    p.write_text("".join(f"v {x} {y} 0\n" for x, y in verts) + "vt 0 0\n" +
+                 "f " + " ".join(f"{i + 1}/1" for i in range(8)) + "\n" + "f 1 2 3 4\n")
+    _, corners = fsamd.load_obj(str(p))
+    tris = [tuple(c[0::3]) for c in corners]
+    assert tris == [(0, 1, 2), (0, 2, 3), (0, 3, 4), (4, 5, 6), (4, 6, 7), (0, 4, 7),
+                    (0, 1, 2), (0, 2, 3)]  # then the convex quad
+    assert (corners[:6, 2::3] == 0).all() and (corners[:, 1::3] == -1).all()  # vt kept, no vn
