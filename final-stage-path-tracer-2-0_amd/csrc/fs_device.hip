@@ -268,7 +268,21 @@ __device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, 
 template <bool COUNT>
 struct Tally {
   uint32_t nodes = 0, tris = 0, prims = 0;
+#ifdef FS_PHASE_PROF
+  // wave-level loop trips, counted by the first active lane of each trip
+  uint32_t node_trips = 0, leaf_trips = 0, lane_nodes = 0, lane_leaves = 0;
+#endif
 };
+#ifdef FS_PHASE_PROF
+#define FS_WAVE_TRIP(field)                                                            \
+  do {                                                                                 \
+    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) field++; \
+  } while (0)
+#else
+#define FS_WAVE_TRIP(field) \
+  do {                      \
+  } while (0)
+#endif
 
 // Traverses one mesh's BVH2 (conservative culling) and applies the
 // reference leaf rule: a face replaces the current hit iff t < best, or on an
@@ -997,6 +1011,14 @@ struct MinHit {
   int32_t tc;  // last object that wrote surface_texcoords (-1: still vector2())
 };
 
+// A BVH walk parked mid-way (SUSP schedule): the object it belongs to, the
+// current node, the parked leaf and the stack depth; the stack entries stay
+// in the lane's LDS column and the hit record in its MinHit.
+struct WalkSuspend {
+  int32_t oi = -1;  // -1: no suspended walk
+  uint32_t w = 0, leaf = 0, sp = 0;
+};
+
 // BVH2 traversal of one mesh, closest-hit bookkeeping only (no point/normal).
 template <bool COUNT>
 __device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
@@ -1122,9 +1144,15 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
   }
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
-                                            MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
+// SUSP: when at most `thr` lanes are still walking while other live lanes of
+// the wave wait, the walkers park (state to *ws) and return true; the wave
+// moves on and they resume from *ws in a later iteration (same operations in
+// the same order per lane).
+template <bool COUNT, bool SUSP = false>
+__device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
+                                            MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally,
+                                            WalkSuspend* ws = nullptr, bool resume = false, uint32_t thr = 0,
+                                            uint32_t live = 0) {
   constexpr uint32_t kNone = 0x7FFFFFFFu;  // empty-stack sentinel (no leaf bit, never a node index)
   const float tiny = 1e-20f;
   float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
@@ -1136,13 +1164,24 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
   float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
   float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
   uint32_t w = root, leaf = 0, sp = 0;
+  if (SUSP && resume) {
+    w = ws->w;
+    leaf = ws->leaf;
+    sp = ws->sp;
+  }
   float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;  // h.t only changes in the leaf tests
-  while (w != kNone || leaf) {
+  uint32_t trips = 0;
+  bool susp = false;
+  while ((w != kNone || leaf) && !(SUSP && susp)) {
     while (!(w & kLeafBit) && w != kNone) {
       const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
       float4 X = q[0], Y = q[1], Z = q[2];
       uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       if (COUNT) tally.nodes++;
+#ifdef FS_PHASE_PROF
+      FS_WAVE_TRIP(tally.node_trips);
+      tally.lane_nodes++;
+#endif
       bool h0, h1;
       float t0, t1;
       if (!zl) {
@@ -1181,8 +1220,20 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
         w = sp ? stk[--sp * kBlock] : kNone;
       }
       if (__ballot(leaf == 0) == 0) break;  // every active lane holds a leaf
+      if (SUSP && (++trips & 7u) == 0u) {  // checked every 8 node trips
+        const uint32_t walkers = (uint32_t)__popcll(__builtin_amdgcn_read_exec());
+        if (walkers <= thr && walkers < live) {
+          susp = true;
+          break;
+        }
+      }
     }
+    if (SUSP && susp) break;
     while (leaf) {
+#ifdef FS_PHASE_PROF
+      FS_WAVE_TRIP(tally.leaf_trips);
+      tally.lane_leaves++;
+#endif
       test_leaf<COUNT>(S, leaf, oi, r, zl, h, tally);
       leaf = 0;
       if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
@@ -1192,6 +1243,13 @@ __device__ __forceinline__ void traverse_ww(const DevScene& S, uint32_t root, in
     }
     tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
   }
+  if (SUSP && susp) {
+    ws->oi = oi;
+    ws->w = w;
+    ws->leaf = leaf;
+    ws->sp = sp;
+  }
+  return SUSP && susp;
 }
 
 // Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
@@ -1324,28 +1382,46 @@ struct PhaseAcc {};
 #define FS_TICK() 0ull
 #endif
 
-template <bool COUNT, bool WW = false, bool WIDE = false, bool TEX = false>
+// SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
+// resume it in a later call with the same ray: objects before the parked one
+// are skipped on resume (already processed), the rest follow in order.
+template <bool COUNT, bool WW = false, bool WIDE = false, bool TEX = false, bool SUSP = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
-                                                PhaseAcc& pa, uint32_t* __restrict__ ovf = nullptr) {
-  h.t = 2.0f;
-  h.obj = -1;
-  h.prim = 0;
-  h.u = h.v = 0.0f;
-  h.point = 0;
-  h.tc = -1;
+                                                PhaseAcc& pa, uint32_t* __restrict__ ovf = nullptr,
+                                                WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
+                                                bool* parked = nullptr) {
+  bool resuming = SUSP && ws->oi >= 0;
+  if (!resuming) {
+    h.t = 2.0f;
+    h.obj = -1;
+    h.prim = 0;
+    h.u = h.v = 0.0f;
+    h.point = 0;
+    h.tc = -1;
+  }
   bool zl = zero_len(r);
+  const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
+  bool park = false;
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
+    if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     int32_t kind = o->kind;
     const __attribute__((address_space(4))) float* d = o->d;
     if (kind == FS_OBJ_MESH) {
       if (!o->i2) continue;
       uint64_t t0 = FS_TICK();
-      bool visit = ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
+      const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
+      bool visit = resume_here || ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
       uint64_t t1 = FS_TICK();
-      if (visit) {
+      if (SUSP) {
+        if (visit)
+          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
+                                          o->i5 ? susp_thr : 0u, live);
+        if (resume_here) resuming = false;
+        if (park) continue;
+      } else if (visit) {
         if (WIDE && o->i3 >= 0)
           traverse4_ww<COUNT>(S, (uint32_t)o->i3, (int32_t)oi, r, zl, h, LaneStack{stk, ovf}, tally);
         else if (WW)
@@ -1423,6 +1499,10 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #ifdef FS_PHASE_PROF
     pa.prim += FS_TICK() - tp0;
 #endif
+  }
+  if (SUSP) {
+    if (!park) ws->oi = -1;
+    *parked = park;
   }
 }
 
@@ -1828,7 +1908,8 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false, bool POOL = false>
+template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false, bool POOL = false,
+          bool SUSP = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
@@ -1888,6 +1969,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   uint32_t depth = 0, mats_lo = 0, mats_hi = 0;
   int top = -1;
   bool fresh = true;
+  MinHit h;         // persists across iterations while a walk is parked (SUSP)
+  WalkSuspend ws;
 #ifdef FS_PHASE_PROF
   uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tk = __builtin_readcyclecounter(), t_begin = tk;
@@ -1939,20 +2022,34 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       L = mk3(1, 1, 1);
       done = true;
     } else {
-      segments++;
-      MinHit h;
+      if (!SUSP || ws.oi < 0) segments++;
+      bool parked = false;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW, WIDE, TEX>(S, r, h, stk, tally, pa, ovf);
+      const uint32_t nodes_before = tally.lane_nodes;
+      scene_trace_min<COUNT, WW, WIDE, TEX, SUSP>(S, r, h, stk, tally, pa, ovf, &ws, P.susp_thr, &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
+      {  // histogram of node visits per traced segment: 0,1-4,5-8,9-16,17-32,33-64,65-128,>128
+        uint32_t nv = tally.lane_nodes - nodes_before, bin = 0;
+        if (nv > 0) bin = 1;
+        if (nv > 4) bin = 2;
+        if (nv > 8) bin = 3;
+        if (nv > 16) bin = 4;
+        if (nv > 32) bin = 5;
+        if (nv > 64) bin = 6;
+        if (nv > 128) bin = 7;
+        atomicAdd(&counters->phase[16 + bin], 1ull);
+      }
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW, WIDE, TEX>(S, r, h, stk, tally, pa, ovf);
+      scene_trace_min<COUNT, WW, WIDE, TEX, SUSP>(S, r, h, stk, tally, pa, ovf, &ws, P.susp_thr, &parked);
 #endif
       FS_PHASE(2);
-      if (h.obj < 0) {
+      if (SUSP && parked) {
+        // the walk is parked; the lane resumes it next iteration
+      } else if (h.obj < 0) {
         if (depth == 1) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
         L = mk3(S.sky_r, S.sky_g, S.sky_b);
         if (TEX && S.sky_tex) {  // textured Light sky: SampleSky (scene.cpp:157-162, engine.cpp:91-92)
@@ -2049,6 +2146,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   ph[9] = __builtin_readcyclecounter() - t_begin;
   if (lane == 0)
     for (int i = 0; i < 10; i++) atomicAdd(&counters->phase[i], (unsigned long long)ph[i]);
+  atomicAdd(&counters->phase[10], (unsigned long long)tally.node_trips);
+  atomicAdd(&counters->phase[11], (unsigned long long)tally.leaf_trips);
+  atomicAdd(&counters->phase[12], (unsigned long long)tally.lane_nodes);
+  atomicAdd(&counters->phase[13], (unsigned long long)tally.lane_leaves);
 #endif
 #undef FS_PHASE
   if (POOL) {
@@ -2220,6 +2321,7 @@ struct fs_context {
   DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send,
       pack_recv, range_io;
   bool has_textures = false;
+  bool has_parking = false;  // a mesh of >= kParkMinTris triangles: the SUSP schedule
   DevScene scene{};
   uint32_t num_objects = 0;
   PreparedScene host;
@@ -2388,19 +2490,21 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   return FS_OK;
 }
 
-enum class KernelMode { kLean, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
+enum class KernelMode { kAuto, kLean, kLeanSusp, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
 
 KernelMode kernel_mode() {
   const char* e = std::getenv("FS_KERNEL");
-  if (!e || !*e) return KernelMode::kLean;
+  if (!e || !*e) return KernelMode::kAuto;
   std::string m(e);
   if (m == "regen") return KernelMode::kRegen;
   if (m == "lean_ifif") return KernelMode::kLeanIfIf;
   if (m == "lean_bvh4") return KernelMode::kLeanBvh4;
   if (m == "lean_nopool") return KernelMode::kLeanNoPool;
+  if (m == "lean_susp") return KernelMode::kLeanSusp;
+  if (m == "lean") return KernelMode::kLean;
   if (m == "lockstep") return KernelMode::kLockstep;
   if (m == "wavefront") return KernelMode::kWavefront;
-  return KernelMode::kLean;
+  return KernelMode::kAuto;
 }
 
 }  // namespace
@@ -2505,6 +2609,8 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   S.sky_tex = (sky.kind == FS_MAT_LIGHT && sky.texture >= 0) ? 1 : 0;
   ctx->has_textures = false;
   for (const fs_material& m : P.materials) ctx->has_textures |= m.texture >= 0;
+  ctx->has_parking = false;
+  for (const DevObject& o : P.objects) ctx->has_parking |= o.kind == FS_OBJ_MESH && o.i5 != 0;
   ctx->num_objects = S.num_objects;
   ctx->host = std::move(P);
   ctx->have_scene = true;
@@ -2611,6 +2717,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_offset = params->tile_offset;
   L.tile_stride = stride;
   L.seed = params->seed;
+  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 16u;
+  L.pad = 0;
   uint32_t owned = params->tile_offset < tiles ? (tiles - params->tile_offset + stride - 1) / stride : 0;
   uint64_t blocks = (uint64_t)owned * (ts / 8) * (ts / 8);
   DevCamera C = camera_basis(camera, params->width, params->height);
@@ -2620,15 +2728,21 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // pixel; the running mean lives in the frame, so the result is identical.
   const uint32_t chunk = kChunk;
   // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
-  // produces identical frames): "lean" (default) path-regeneration megakernel
-  // with the unwind scratch in HBM rows, while-while traversal and the wave's
-  // (pixel, sample) tasks pooled across lanes; "lean_nopool" one pixel per lane;
+  // produces identical frames): "lean" path-regeneration megakernel with the
+  // unwind scratch in HBM rows, while-while traversal and the wave's
+  // (pixel, sample) tasks pooled across lanes; "lean_susp" the same with walks
+  // of large meshes parked when few lanes still walk (the default when the
+  // scene has a mesh of >= kParkMinTris triangles, else "lean");
+  // "lean_nopool" one pixel per lane;
   // "lean_bvh4" with 4-wide nodes for scenes uploaded with FS_BVH4=1 (slower:
   // more VALU per step); "lean_ifif" the single-loop traversal; "regen" with the unwind
   // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
   // extend/shade kernels over a compacted path queue.
-  const KernelMode mode = kernel_mode();
-  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanNoPool && mode != KernelMode::kLeanBvh4 &&
+  KernelMode mode = kernel_mode();
+  if (mode == KernelMode::kAuto)
+    mode = ctx->has_parking && !ctx->has_textures ? KernelMode::kLeanSusp : KernelMode::kLean;
+  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanSusp && mode != KernelMode::kLeanNoPool &&
+      mode != KernelMode::kLeanBvh4 &&
       mode != KernelMode::kLeanIfIf)
     return fail(FS_ERR_INVALID, "textured scenes need the default (lean) kernel schedule");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
@@ -2685,7 +2799,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     return FS_OK;
   }
   dev::WfState lean{};
-  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanNoPool || mode == KernelMode::kLeanBvh4 ||
+  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanSusp ||
+                         mode == KernelMode::kLeanNoPool || mode == KernelMode::kLeanBvh4 ||
                          mode == KernelMode::kLeanIfIf;
   if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
     if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean, ctx->has_textures))) return rc;
@@ -2704,6 +2819,9 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
                    : dev::render_kernel_lean<false, 6, true, false, true, true>;
       else if (mode == KernelMode::kLeanNoPool)
         lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
+      else if (mode == KernelMode::kLeanSusp)
+        lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true, true>
+                   : dev::render_kernel_lean<false, 6, true, false, false, true, true>;
       else if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
       else if (mode == KernelMode::kLeanIfIf)
@@ -2756,6 +2874,14 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                "shade %llu unwind %llu - iters %llu total %llu\n",
                c.phase[0], c.phase[1], c.phase[2], c.phase[5], c.phase[6], c.phase[7], c.phase[3], c.phase[4],
                c.phase[8], c.phase[9]);
+  std::fprintf(stderr,
+               "[fs trips] node loop: %llu wave trips, %llu lane visits (%.1f%% of lanes); leaf loop: %llu wave "
+               "trips, %llu lane leaves (%.1f%%)\n",
+               c.phase[10], c.phase[12], 100.0 * c.phase[12] / (64.0 * (c.phase[10] ? c.phase[10] : 1)), c.phase[11],
+               c.phase[13], 100.0 * c.phase[13] / (64.0 * (c.phase[11] ? c.phase[11] : 1)));
+  std::fprintf(stderr, "[fs hist] node visits per segment: 0:%llu 1-4:%llu 5-8:%llu 9-16:%llu 17-32:%llu 33-64:%llu "
+               "65-128:%llu >128:%llu\n", c.phase[16], c.phase[17], c.phase[18], c.phase[19], c.phase[20],
+               c.phase[21], c.phase[22], c.phase[23]);
 #endif
   return FS_OK;
 }

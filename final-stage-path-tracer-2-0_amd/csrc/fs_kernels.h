@@ -57,12 +57,14 @@ struct DevCounters {
   unsigned long long samples, segments, node_visits, tri_tests, prim_tests;
   // Per-wave cycle totals by loop phase; filled only by -DFS_PHASE_PROF
   // builds (libfsgpu_prof.so, a measurement tool, never the product path).
-  unsigned long long phase[10];
+  unsigned long long phase[32];
 };
 
 struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;
   uint32_t sample_base, spp;
+  uint32_t susp_thr;  // SUSP schedule: park walks when at most this many lanes still walk
+  uint32_t pad;
   uint64_t seed;
 };
 

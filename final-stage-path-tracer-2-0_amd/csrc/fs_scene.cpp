@@ -821,6 +821,10 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
     mesh_out[mi].root4 = use4 ? Collapse4(S.nodes, &S.nodes4).run(mesh_out[mi].root) : -1;
   }
 
+  // FS_PARK_MIN_TRIS lowers the parking threshold (tests exercise the SUSP
+  // schedule on small meshes with it).
+  const char* pe = std::getenv("FS_PARK_MIN_TRIS");
+  const uint32_t park_min = pe ? (uint32_t)std::strtoul(pe, nullptr, 10) : kParkMinTris;
   S.objects.resize(d->num_objects);
   for (uint32_t i = 0; i < d->num_objects; i++) {
     const fs_object& o = d->objects[i];
@@ -843,6 +847,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       D.i2 = mo.tree ? 1 : 0;
       D.i3 = mo.tree ? mo.root4 : -1;
       D.i4 = mo.texcoords ? 1 : 0;
+      D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);
       put3(D.d + 3, mo.rb.mx);
     } else {

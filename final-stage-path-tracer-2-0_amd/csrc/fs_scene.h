@@ -14,6 +14,12 @@ namespace fs {
 
 // Object record, 192 B; read wave-uniformly by the object loop of
 // Scene::Trace (scene.cpp:231-233), so it is fetched with scalar loads.
+// Meshes at least this large let their BVH walks park under the SUSP
+// schedule (fs_device.hip): measured on MI355X, parking pays for the ~1M
+// triangle C4 blob (+15%) and loses on the ~250k-triangle C3 atrium (-4%,
+// meshes of 60-120k triangles), so only scenes with such a mesh select it.
+constexpr uint32_t kParkMinTris = 1u << 19;
+
 struct DevObject {
   int32_t kind;  // fs_object_kind (QUAD_PUV is stored as QUAD_ONWH)
   int32_t mat;
@@ -22,7 +28,7 @@ struct DevObject {
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
   int32_t i3;    // MESH: BVH4 root node index, or -1 (traverse the BVH2)
   int32_t i4;    // MESH: 1 if the mesh has texcoords (mesh.cpp:300)
-  int32_t i5;
+  int32_t i5;    // MESH: 1 if its walks may park (>= kParkMinTris triangles, SUSP schedule)
   float d[40];
   // SPHERE  d0-2 center, d3 radius
   // PLANE   d0-3 plane

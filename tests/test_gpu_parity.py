@@ -83,6 +83,20 @@ def test_scene_parity(name, dims, scene_dir, gpu_renderer):
     assert_parity(out, ref, exact=True)
 
 
+@pytest.mark.parametrize("name,dims", [("c3", (96, 54, 4)), ("c2", (96, 54, 8))])
+def test_parked_walks_bit_exact(name, dims, scene_dir, gpu_renderer, monkeypatch):
+    """The SUSP schedule (walks of large meshes park while few lanes walk and
+    resume on a later iteration) changes no result: with the threshold
+    lowered every mesh may park; frames stay bit-exact with the oracle."""
+    W, H, spp = dims
+    monkeypatch.setenv("FS_PARK_MIN_TRIS", "1")
+    monkeypatch.setenv("FS_KERNEL", "lean_susp")
+    s = load_scene(name, scene_dir)
+    out = gpu_render(gpu_renderer, s, s.camera(0), W, H, spp)
+    ref = oracle_render(s.desc_ptr(), s.camera(0), W, H, spp)
+    assert_parity(out, ref, exact=True)
+
+
 def zoo(frost=0.0):
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
