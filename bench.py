@@ -128,6 +128,7 @@ def main():
     r.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    kernel_name = r.last_kernel()
     if dist:
         import torch
 
@@ -160,7 +161,7 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "render_kernel_lean<false, 6, true, false, false, true>", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "bytes_per_sample": round(bytes_per_sample, 1),
                 "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
                 "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),

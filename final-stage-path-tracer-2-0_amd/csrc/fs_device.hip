@@ -2322,6 +2322,7 @@ struct fs_context {
       pack_recv, range_io;
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= kParkMinTris triangles: the SUSP schedule
+  const char* last_kernel = "";  // the trace kernel the last fs_render launched
   DevScene scene{};
   uint32_t num_objects = 0;
   PreparedScene host;
@@ -2808,24 +2809,36 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
+    // (names as rocprofv3 prints the uncounted instantiations, for fs_last_kernel)
     auto kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
-    if (mode == KernelMode::kLockstep) kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
+    ctx->last_kernel = "render_kernel_regen<false, 4>";
+    if (mode == KernelMode::kLockstep) {
+      kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
+      ctx->last_kernel = "render_kernel<false>";
+    }
     if (lean_mode) {
       // default: while-while BVH2 traversal, pooled (pixel, sample) tasks
       auto lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true>
                       : dev::render_kernel_lean<false, 6, true, false, false, true>;
-      if (ctx->has_textures)  // textured scenes: the instantiation with texcoords + texel rows
+      ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, false>";
+      if (ctx->has_textures) {  // textured scenes: the instantiation with texcoords + texel rows
         lk = count ? dev::render_kernel_lean<true, 6, true, false, true, true>
                    : dev::render_kernel_lean<false, 6, true, false, true, true>;
-      else if (mode == KernelMode::kLeanNoPool)
+        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, true, true, false>";
+      } else if (mode == KernelMode::kLeanNoPool) {
         lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
-      else if (mode == KernelMode::kLeanSusp)
+        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, false, false>";
+      } else if (mode == KernelMode::kLeanSusp) {
         lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true, true>
                    : dev::render_kernel_lean<false, 6, true, false, false, true, true>;
-      else if (mode == KernelMode::kLeanBvh4)  // needs a scene uploaded with FS_BVH4=1
+        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, true>";
+      } else if (mode == KernelMode::kLeanBvh4) {  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
-      else if (mode == KernelMode::kLeanIfIf)
+        ctx->last_kernel = "render_kernel_lean<false, 6, true, true, false, false, false>";
+      } else if (mode == KernelMode::kLeanIfIf) {
         lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
+        ctx->last_kernel = "render_kernel_lean<false, 6, false, false, false, false, false>";
+      }
       hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
                          lean.p0, lean.ovf, lean.tex, lean.rad, (DevCounters*)ctx->counters.p);
     } else {
@@ -2845,6 +2858,8 @@ int fs_synchronize(fs_context* ctx) {
   FS_HIP(hipStreamSynchronize(ctx->stream));
   return FS_OK;
 }
+
+const char* fs_last_kernel(fs_context* ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int fs_last_render_ms(fs_context* ctx, float* ms) {
   if (!ctx || !ms) return fail(FS_ERR_INVALID, "null argument");

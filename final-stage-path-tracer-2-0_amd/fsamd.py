@@ -107,6 +107,7 @@ GPU_SYMBOLS = {
     "fs_synchronize": ([_VP], C.c_int),
     "fs_read_counters": ([_VP, C.POINTER(fs_counters)], C.c_int),
     "fs_last_render_ms": ([_VP, C.POINTER(C.c_float)], C.c_int),
+    "fs_last_kernel": ([_VP], C.c_char_p),
     "fs_comm_unique_id": ([C.c_char_p], C.c_int),
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
@@ -373,6 +374,10 @@ class Renderer:
         ms = C.c_float()
         _check(gpu_lib().fs_last_render_ms(self.ctx, C.byref(ms)), "fs_last_render_ms")
         return ms.value
+
+    def last_kernel(self):
+        """The trace kernel the last render launched (rocprofv3's name)."""
+        return gpu_lib().fs_last_kernel(self.ctx).decode()
 
     def counters(self):
         c = fs_counters()

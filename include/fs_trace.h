@@ -239,6 +239,10 @@ int fs_synchronize(fs_context* ctx);
 int fs_read_counters(fs_context* ctx, fs_counters* out); /* and zero them */
 /* Device time of the last fs_render's trace kernel(s) in ms (HIP events). */
 int fs_last_render_ms(fs_context* ctx, float* ms);
+/* Name of the trace kernel the last fs_render launched, as rocprofv3 lists it
+ * (the schedule depends on the scene: see DESIGN.md); "" before any render.
+ * Profiling aid, no reference counterpart. */
+const char* fs_last_kernel(fs_context* ctx);
 
 /* ---- multi-GPU (RCCL over xGMI) ---------------------------------------- */
 #define FS_COMM_ID_BYTES 128
