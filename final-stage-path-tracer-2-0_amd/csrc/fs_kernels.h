@@ -64,7 +64,7 @@ struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;
   uint32_t sample_base, spp;
   uint32_t susp_thr;  // SUSP schedule: park walks when at most this many lanes still walk
-  uint32_t pad;
+  uint32_t xcd_bands;  // 1: each XCD (blocks b, b+8, ...) renders one contiguous band of micro-tiles
   uint64_t seed;
 };
 

@@ -156,7 +156,12 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
   t->plane[3] = pl.w;
 }
 
-constexpr int kBins = 16;
+constexpr int kMaxBins = 64;
+// SAH bins per axis (FS_BVH_BINS overrides, for tuning).
+int bins_env() {
+  int v = std::getenv("FS_BVH_BINS") ? std::atoi(std::getenv("FS_BVH_BINS")) : 16;
+  return (v >= 2 && v <= kMaxBins) ? v : 16;
+}
 // Target leaf size (FS_BVH_LEAF overrides, for tuning).
 uint32_t leaf_target_env() {
   uint32_t v = std::getenv("FS_BVH_LEAF") ? (uint32_t)std::atoi(std::getenv("FS_BVH_LEAF")) : 2u;
@@ -278,19 +283,19 @@ class BvhBuilder {
       for (int ax = 0; ax < 3; ax++) {
         float ext = cmax[ax] - cmin[ax];
         if (!(ext > 0.0f)) continue;
-        Box bb[kBins];
-        uint32_t bc[kBins] = {0};
-        float scale = kBins / ext;
+        Box bb[kMaxBins];
+        uint32_t bc[kMaxBins] = {0};
+        float scale = bins_ / ext;
         for (uint32_t i = b; i < e; i++) {
-          int k = std::min(kBins - 1, (int)((P[i].c[ax] - cmin[ax]) * scale));
+          int k = std::min(bins_ - 1, (int)((P[i].c[ax] - cmin[ax]) * scale));
           bb[k].grow(P[i].box);
           bc[k]++;
         }
-        Box left[kBins];
-        uint32_t lc[kBins];
+        Box left[kMaxBins];
+        uint32_t lc[kMaxBins];
         Box acc;
         uint32_t cnt = 0;
-        for (int k = 0; k < kBins; k++) {
+        for (int k = 0; k < bins_; k++) {
           acc.grow(bb[k]);
           cnt += bc[k];
           left[k] = acc;
@@ -298,7 +303,7 @@ class BvhBuilder {
         }
         Box racc;
         uint32_t rcnt = 0;
-        for (int k = kBins - 1; k > 0; k--) {
+        for (int k = bins_ - 1; k > 0; k--) {
           racc.grow(bb[k]);
           rcnt += bc[k];
           if (lc[k - 1] == 0 || rcnt == 0) continue;
@@ -312,9 +317,9 @@ class BvhBuilder {
       }
       if (best_axis >= 0) {
         float ext = cmax[best_axis] - cmin[best_axis];
-        float scale = kBins / ext;
+        float scale = bins_ / ext;
         auto mid = std::partition(P.begin() + b, P.begin() + e, [&](const Prim& p) {
-          int k = std::min(kBins - 1, (int)((p.c[best_axis] - cmin[best_axis]) * scale));
+          int k = std::min(bins_ - 1, (int)((p.c[best_axis] - cmin[best_axis]) * scale));
           return k < best_bin;
         });
         uint32_t m = (uint32_t)(mid - P.begin());
@@ -339,6 +344,7 @@ class BvhBuilder {
     L->b.reset(new BvhBuilder(&L->nodes, &L->tris, &L->normals, &L->tex, mesh_tris_, mesh_normals_, mesh_tex_));
     L->b->prims_ = prims_;
     L->b->leaf_ = leaf_;
+    L->b->bins_ = bins_;
     L->b->par_depth_ = par_depth_;
   }
   // Appends a local subtree after everything built so far: the result is the
@@ -411,6 +417,7 @@ class BvhBuilder {
   const std::vector<float>* mesh_tex_;
   std::vector<Prim>* prims_ = nullptr;
   uint32_t leaf_ = leaf_target_env();
+  int bins_ = bins_env();
   uint32_t par_depth_ = parallel_depth_env();
   uint32_t max_depth_ = 0;
   bool overflow_ = false;

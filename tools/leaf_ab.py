@@ -1,4 +1,5 @@
-"""A/B of BVH leaf sizes (FS_BVH_LEAF) in one process: rebuild + time."""
+"""A/B of BVH build settings in one process: rebuild + time.
+usage: python tools/leaf_ab.py VALUES scenes [spp] [ENV]   (ENV default FS_BVH_LEAF; e.g. FS_BVH_BINS)"""
 import os
 import sys
 import time
@@ -13,6 +14,7 @@ import scenes  # noqa: E402
 leaves = sys.argv[1].split(",")
 names = sys.argv[2].split(",")
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+env = sys.argv[4] if len(sys.argv) > 4 else "FS_BVH_LEAF"
 W, H = 1920, 1080
 for name in names:
     p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
@@ -24,7 +26,7 @@ for name in names:
     f = r.frame(W, H)
     ref = None
     for lf in leaves:
-        os.environ["FS_BVH_LEAF"] = lf
+        os.environ[env] = lf
         r.upload(s)
         st = r.scene_stats()
         ms = []
@@ -36,5 +38,5 @@ for name in names:
         same = ref is None or np.array_equal(img, ref)
         ref = img if ref is None else ref
         m = float(np.median(ms[1:]))
-        print(f"{name} leaf {lf}: nodes {st['nodes']} build {st['build_ms']:.0f} ms  render {m:.1f} ms "
+        print(f"{name} {env}={lf}: nodes {st['nodes']} build {st['build_ms']:.0f} ms  render {m:.1f} ms "
               f"{W*H*spp/m/1e3:.1f} Msamples/s  same-as-first={same}", flush=True)
