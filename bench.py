@@ -129,6 +129,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t_start
     kernel_name = r.last_kernel()
+    launches, launch_spp = r.last_launches()
     if dist:
         import torch
 
@@ -146,22 +147,23 @@ def main():
     cf.close()
     bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * c["tri_tests"] + S_PRIM * c["prim_tests"]
                         + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
-    chunk = 32  # fs_render splits a step into launches of 32 spp (fs_device.hip)
-    launches = (spp + chunk - 1) // chunk
     avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
     owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
     per_launch_bytes = bytes_per_sample * owned_samples / launches
     achieved = per_launch_bytes / avg_launch_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}.json")
-    if os.path.exists(pmc) and spp == 1024:
+    if os.path.exists(pmc):  # PMC passes of tools/gpu_pmc.sh, per sample of the same kernel
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pm = json.load(open(pmc))
+            if kernel_name in pm.get("kernel", "") and pm.get("hbm_bytes_per_sample"):
+                traffic = round(pm["hbm_bytes_per_sample"] * owned_samples / launches)
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "launches_per_step": launches, "spp_per_launch": launch_spp,
                 "bytes_per_sample": round(bytes_per_sample, 1),
                 "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
                 "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),

@@ -1932,6 +1932,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   uint32_t x0, y0;  // the wave's 8x8 pixel micro-tile
+  uint32_t group = 0, rad_row = blockIdx.x;  // sample group; radiance row (g * micro-tiles + micro-tile)
   {
     const uint32_t micro_per_side = P.tile_size / 8;
     const uint32_t micro_per_tile = micro_per_side * micro_per_side;
@@ -1947,12 +1948,26 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       const uint32_t xcd = b & 7u, k = b >> 3;
       if (k < groups * micro_per_tile) b = ((k / micro_per_tile) * 8 + xcd) * micro_per_tile + k % micro_per_tile;
     }
-    const uint32_t owned = b / micro_per_tile, micro = b % micro_per_tile;
-    const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+    // a virtual tile list of owned tiles x groups, tile-major (a tile's
+    // groups run together: the resident waves cover few tiles) or, with
+    // group_major, group-major
+    const uint32_t vtile = b / micro_per_tile, micro = b % micro_per_tile;
+    uint32_t t;
+    if (P.group_major) {
+      group = vtile / P.owned;
+      t = vtile - group * P.owned;
+    } else {
+      t = vtile / P.groups;
+      group = vtile - t * P.groups;
+    }
+    rad_row = (group * P.owned + t) * micro_per_tile + micro;
+    const uint32_t tile = P.tile_offset + t * P.tile_stride;
     const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     x0 = tx * P.tile_size + (micro % micro_per_side) * 8;
     y0 = ty * P.tile_size + (micro / micro_per_side) * 8;
   }
+  const uint64_t sample_base = (uint64_t)P.sample_base + (uint64_t)group * P.spp;
+  const bool last_group = group + 1 == P.groups;
   uint32_t x = x0 + (lane & 7), y = y0 + (lane >> 3);
   const bool own_valid = x < F.width && y < F.height;
   if (!POOL && !own_valid) return;
@@ -1970,7 +1985,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   // sample-major order from a wave-uniform counter by whichever lane is
   // free; each sample's radiance goes to a scratch row and every pixel folds
   // its samples in order at the end (same running-mean rounding).
-  float* rad = rad_all + (size_t)blockIdx.x * (3 * kChunk * kBlock);
+  float* rad = rad_all + (size_t)rad_row * (3 * kChunk * kBlock);
   uint32_t next_task = 0;
   // only the micro-tile's in-frame pixels (vx x vy) are enumerated, so every
   // task is real work and the loop has no early continue
@@ -2019,7 +2034,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       next_task += (uint32_t)__popcll(m);
     }
     if (fresh) {
-      rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
+      rng = pixel_seed(pix, sample_base + s, P.seed);
       r = camera_ray(C, (float)x, (float)y, rng);
       depth = 0;
       mats_lo = mats_hi = 0;
@@ -2072,7 +2087,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           sphere_tc(normalize(r.stop - r.start), tu, tv);
           L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
         }
-        if (depth == 0 && (!POOL || s == P.spp - 1)) {  // the last sample's AOVs remain
+        if (depth == 0 && (!POOL || (last_group && s == P.spp - 1))) {  // the last sample's AOVs remain
           f3 nd = normalize(r.dir);
           at_byte(F.normal, pix * 12u)[0] = nd.x;
           at_byte(F.normal, pix * 12u)[1] = nd.y;
@@ -2108,7 +2123,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           mats_hi |= (uint32_t)mi << (8 * (depth - 4));
         top = (int)depth;
         if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
-        if (depth == 0 && (!POOL || s == P.spp - 1)) {
+        if (depth == 0 && (!POOL || (last_group && s == P.spp - 1))) {
           at_byte(F.normal, pix * 12u)[0] = nn.x;
           at_byte(F.normal, pix * 12u)[1] = nn.y;
           at_byte(F.normal, pix * 12u)[2] = nn.z;
@@ -2170,6 +2185,16 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   if (POOL) {
     __syncthreads();  // the wave's radiance rows are complete and visible
     if (!own_valid) return;
+    if (P.groups > 1) {  // fold_groups folds every group's rows in sample order
+      if (COUNT) {
+        atomicAdd(&counters->samples, (unsigned long long)P.spp);
+        atomicAdd(&counters->segments, (unsigned long long)segments);
+        atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+        atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+        atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+      }
+      return;
+    }
     x = x0 + (lane & 7);
     y = y0 + (lane >> 3);
     pix = y * F.width + x;
@@ -2197,6 +2222,42 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
     atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
   }
+}
+
+// Folds the radiance rows of a launch with P.groups > 1 into the frame:
+// block b is micro-tile b of group 0 (same decode as render_kernel_lean with
+// xcd_bands 0), lane = pixel; group g's rows are row g * gridDim.x + b. Each
+// pixel folds its samples in sample order (frame.cpp:53-63), so the frame is
+// bit-identical to groups x spp consecutive single-group launches. HBM-bound:
+// 12 B read per sample plus one frame row.
+__global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, const float* __restrict__ rad_all) {
+  const uint32_t lane = threadIdx.x, b = blockIdx.x;
+  const uint32_t micro_per_side = P.tile_size / 8, micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t owned = b / micro_per_tile, micro = b % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t x = (tile % P.tiles_x) * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+  const uint32_t y = (tile / P.tiles_x) * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  if (x >= F.width || y >= F.height) return;
+  const size_t pix = (size_t)y * F.width + x;
+  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
+  uint32_t n = F.count[pix];
+  for (uint32_t g = 0; g < P.groups; g++) {
+    const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * kChunk * kBlock);
+    for (uint32_t k = 0; k < P.spp; k++) {
+      const uint32_t o = k * kBlock + lane;
+      f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
+      f3 np = mean * (float)n + L;
+      float dv = (float)(++n);
+      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+    }
+  }
+  F.color[3 * pix] = mean.x;
+  F.color[3 * pix + 1] = mean.y;
+  F.color[3 * pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * pix] = gamma8(mean.x);
+  F.display[3 * pix + 1] = gamma8(mean.y);
+  F.display[3 * pix + 2] = gamma8(mean.z);
 }
 
 // TraceRange (engine.cpp:298-329): one query per lane, the camera ray through
@@ -2338,6 +2399,8 @@ struct fs_context {
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= kParkMinTris triangles: the SUSP schedule
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
+  uint32_t last_launches = 0;    // trace-kernel launches of the last fs_render
+  uint32_t last_launch_spp = 0;  // samples per pixel of its largest launch
   DevScene scene{};
   uint32_t num_objects = 0;
   PreparedScene host;
@@ -2418,10 +2481,15 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 }
 
 // Carves the wavefront state for `slots` paths out of one allocation.
-int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = false) {
-  size_t per = 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 + 4 +
-               4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
-  size_t bytes = (size_t)slots * per + 64 * 32 + 1024;
+// The lean kernels use only the shading rows (lvl), the Fog anchors (p0),
+// the BVH4 overflow stack (ovf, lean_bvh4 only), texel rows and radiance rows.
+int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = false, bool lean = false,
+             bool ovf_rows = true) {
+  size_t per = lean ? 8 * kMaxDepth + 32 + (ovf_rows ? 4 * kStackOverflow : 0) + (tex_rows ? 16 * kMaxDepth : 0) +
+                          12 * kChunk
+                    : 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 +
+                          4 + 4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
+  size_t bytes = (size_t)slots * per + 64 * 32 + 256 * 24;  // + alignment of each array
   if (ctx->wf.bytes < bytes) {
     int rc = ensure(&ctx->wf, bytes);
     if (rc) return rc;
@@ -2432,7 +2500,17 @@ int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = f
     p += (n + 255) & ~(size_t)255;
     return q;
   };
+  *W = dev::WfState{};
   W->count = (uint32_t*)take(64);
+  if (lean) {
+    W->p0 = (float4*)take(32ull * slots);
+    W->lvl = (float2*)take(8ull * kMaxDepth * slots);
+    W->ovf = ovf_rows ? (uint32_t*)take(4ull * kStackOverflow * slots) : nullptr;
+    W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
+    W->rad = (float*)take(12ull * kChunk * slots);
+    if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
+    return FS_OK;
+  }
   W->pixel = (uint32_t*)take(4ull * slots);
   W->ray0 = (float4*)take(16ull * slots);
   W->ray1 = (float4*)take(16ull * slots);
@@ -2725,7 +2803,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   int rc = check_params(params, frame, &ts, &stride);
   if (rc) return rc;
   if ((rc = set_device(ctx))) return rc;
-  Launch L;
+  Launch L{};
   L.tile_size = ts;
   L.tiles_x = (params->width + ts - 1) / ts;
   uint32_t tiles_y = (params->height + ts - 1) / ts;
@@ -2820,12 +2898,38 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanSusp ||
                          mode == KernelMode::kLeanNoPool || mode == KernelMode::kLeanBvh4 ||
                          mode == KernelMode::kLeanIfIf;
-  if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
-    if ((rc = wf_state(ctx, (uint32_t)(blocks * kBlock), &lean, ctx->has_textures))) return rc;
+  // Sample groups (pooled lean kernels only): a launch renders G runs of
+  // `chunk` samples as G x blocks blocks, then fold_groups folds them in
+  // order. G is sized so a launch holds >= kGroupTargetBlocks blocks (about
+  // 20 waves per wave slot of the chip), which makes the launch tail small
+  // and keeps the CUs full when a multi-GPU rank owns few tiles.
+  const bool pooled = lean_mode && (ctx->has_textures || mode == KernelMode::kLean || mode == KernelMode::kLeanSusp);
+  const uint32_t full_chunks = params->spp / chunk;
+  uint32_t G = 1;
+  if (pooled && blocks && full_chunks > 1) {
+    uint64_t want = (kGroupTargetBlocks + blocks - 1) / blocks;
+    if (const char* e = std::getenv("FS_GROUPS")) want = (uint64_t)std::max(1, std::atoi(e));
+    want = std::min<uint64_t>(want, full_chunks);
+    const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
+    G = (full_chunks + nl - 1) / nl;                                   // balanced groups per launch
   }
-  for (uint32_t done = 0; done < params->spp && blocks; done += chunk) {
+  L.owned = owned;
+  L.groups = 1;
+  L.group_major = std::getenv("FS_GROUP_ORDER") ? (uint32_t)std::atoi(std::getenv("FS_GROUP_ORDER")) : 0u;
+  ctx->last_launches = 0;
+  ctx->last_launch_spp = 0;
+  if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
+    if ((rc = wf_state(ctx, (uint32_t)(blocks * G * kBlock), &lean, ctx->has_textures, true,
+                       mode == KernelMode::kLeanBvh4)))
+      return rc;
+  }
+  for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
+    L.groups = L.spp == chunk ? std::min(G, (params->spp - done) / chunk) : 1u;
+    done += L.groups * L.spp;
+    ctx->last_launches++;
+    ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
     // (names as rocprofv3 prints the uncounted instantiations, for fs_last_kernel)
     auto kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
     ctx->last_kernel = "render_kernel_regen<false, 4>";
@@ -2856,8 +2960,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
         ctx->last_kernel = "render_kernel_lean<false, 6, false, false, false, false, false>";
       }
-      hipLaunchKernelGGL(lk, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, lean.lvl,
-                         lean.p0, lean.ovf, lean.tex, lean.rad, (DevCounters*)ctx->counters.p);
+      hipLaunchKernelGGL(lk, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
+                         lean.lvl, lean.p0, lean.ovf, lean.tex, lean.rad, (DevCounters*)ctx->counters.p);
+      if (L.groups > 1)
+        hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, lean.rad);
     } else {
       hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
                          (DevCounters*)ctx->counters.p);
@@ -2877,6 +2983,13 @@ int fs_synchronize(fs_context* ctx) {
 }
 
 const char* fs_last_kernel(fs_context* ctx) { return ctx ? ctx->last_kernel : ""; }
+
+int fs_last_render_launches(fs_context* ctx, uint32_t* launches, uint32_t* spp_per_launch) {
+  if (!ctx || !launches || !spp_per_launch) return fail(FS_ERR_INVALID, "null argument");
+  *launches = ctx->last_launches;
+  *spp_per_launch = ctx->last_launch_spp;
+  return FS_OK;
+}
 
 int fs_last_render_ms(fs_context* ctx, float* ms) {
   if (!ctx || !ms) return fail(FS_ERR_INVALID, "null argument");

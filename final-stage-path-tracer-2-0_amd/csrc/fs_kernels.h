@@ -14,7 +14,10 @@
 namespace fs {
 
 constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS columns
-constexpr uint32_t kChunk = 32;  // samples per pixel per launch (fs_render splits longer renders)
+constexpr uint32_t kChunk = 32;  // samples per pixel per block (fs_render splits longer renders)
+// fs_render sizes sample groups so one launch holds at least this many blocks
+// (~21 per wave slot of 256 CUs x 24 waves).
+constexpr uint64_t kGroupTargetBlocks = 131072;
 
 struct DevScene {
   const DevObject* __restrict__ objects;
@@ -65,6 +68,14 @@ struct Launch {
   uint32_t sample_base, spp;
   uint32_t susp_thr;  // SUSP schedule: park walks when at most this many lanes still walk
   uint32_t xcd_bands;  // 1: each XCD (blocks b, b+8, ...) renders one contiguous band of micro-tiles
+  // Sample groups: one launch renders `groups` consecutive runs of `spp`
+  // samples; block (g, micro-tile) takes samples sample_base + g*spp ...
+  // Groups > 1 leave the radiance rows for fold_groups, which folds them into
+  // the frame in sample order (the launch tail and a small multi-GPU share no
+  // longer leave CUs idle).
+  uint32_t groups;
+  uint32_t owned;  // 64x64 tiles this launch renders per group
+  uint32_t group_major;  // block order: 0 a tile's groups together, 1 group by group (A/B)
   uint64_t seed;
 };
 

@@ -108,6 +108,7 @@ GPU_SYMBOLS = {
     "fs_read_counters": ([_VP, C.POINTER(fs_counters)], C.c_int),
     "fs_last_render_ms": ([_VP, C.POINTER(C.c_float)], C.c_int),
     "fs_last_kernel": ([_VP], C.c_char_p),
+    "fs_last_render_launches": ([_VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
     "fs_comm_unique_id": ([C.c_char_p], C.c_int),
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
@@ -378,6 +379,12 @@ class Renderer:
     def last_kernel(self):
         """The trace kernel the last render launched (rocprofv3's name)."""
         return gpu_lib().fs_last_kernel(self.ctx).decode()
+
+    def last_launches(self):
+        """(trace-kernel launches, spp of the largest launch) of the last render."""
+        n, spp = C.c_uint32(), C.c_uint32()
+        _check(gpu_lib().fs_last_render_launches(self.ctx, C.byref(n), C.byref(spp)), "fs_last_render_launches")
+        return n.value, spp.value
 
     def counters(self):
         c = fs_counters()

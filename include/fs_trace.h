@@ -243,6 +243,10 @@ int fs_last_render_ms(fs_context* ctx, float* ms);
  * (the schedule depends on the scene: see DESIGN.md); "" before any render.
  * Profiling aid, no reference counterpart. */
 const char* fs_last_kernel(fs_context* ctx);
+/* Launch shape of the last fs_render: the number of trace-kernel launches and
+ * the samples per pixel of the largest one (renders are cut into launches of
+ * sample groups). Profiling aid, no reference counterpart. */
+int fs_last_render_launches(fs_context* ctx, uint32_t* launches, uint32_t* spp_per_launch);
 
 /* ---- multi-GPU (RCCL over xGMI) ---------------------------------------- */
 #define FS_COMM_ID_BYTES 128

@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh for one kernel.
 
-usage: python tools/pmc_summary.py gpurun_out/<round>/pmc KERNEL_SUBSTR OUT.json [note]
+usage: python tools/pmc_summary.py gpurun_out/<round>/pmc KERNEL_SUBSTR OUT.json [note] [samples_per_launch]
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 128-B read requests at
@@ -18,6 +18,7 @@ from collections import defaultdict
 def main():
     pmc_dir, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
     note = sys.argv[4] if len(sys.argv) > 4 else ""
+    samples = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # samples one launch of the kernel renders
     vals = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
     meta = {}
     for f in sorted(glob.glob(os.path.join(pmc_dir, "*", "*counter_collection.csv"))):
@@ -41,6 +42,9 @@ def main():
         res["fetch_bytes_per_launch"] = fetch
         res["write_bytes_per_launch"] = write
         res["hbm_bytes_per_launch"] = round(fetch + write)
+        if samples:
+            res["samples_per_launch"] = samples
+            res["hbm_bytes_per_sample"] = round((fetch + write) / samples, 2)
     if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
         res["l2_hit_rate"] = round(avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1), 4)
     if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
