@@ -1156,9 +1156,13 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   const bool zl = ZLMODE < 0 ? zl_rt : ZLMODE == 1;
   constexpr uint32_t kNone = 0x7FFFFFFFu;  // empty-stack sentinel (no leaf bit, never a node index)
   const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
+  // A zero-length ray (a point test at the leaves) walks with a 1e-20 slope
+  // per axis: every box that contains the start passes the slab test (entry
+  // <= 0 <= exit), so the cull stays a superset of the point-in-box test
+  // without a per-node branch.
+  float dx = fabsf(r.dir.x) < tiny || zl ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny || zl ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny || zl ? copysignf(tiny, r.dir.z) : r.dir.z;
   // v_rcp (about 1 ulp) instead of IEEE division: the slab test is a
   // conservative cull whose t margins (1e-6 absolute, 2e-6 relative) and
   // box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
@@ -1185,7 +1189,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
 #endif
       bool h0, h1;
       float t0, t1;
-      if (!zl) {
+      {
         float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
         float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
         float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
@@ -1200,11 +1204,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         h1 = n1 <= f1;
         t0 = n0;
         t1 = n1;
-      } else {
-        f3 s = r.start;
-        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
-        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
-        t0 = t1 = 0.0f;
       }
       if (h0 && h1) {
         bool swap = t1 < t0;
@@ -2584,6 +2583,11 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   return FS_OK;
 }
 
+// Waves per SIMD of the default (pooled) lean kernels; other values are A/B builds.
+#ifndef FS_LEAN_WAVES
+#define FS_LEAN_WAVES 6
+#endif
+
 enum class KernelMode { kAuto, kLean, kLeanSusp, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
 
 KernelMode kernel_mode() {
@@ -2940,7 +2944,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     if (lean_mode) {
       // default: while-while BVH2 traversal, pooled (pixel, sample) tasks
       auto lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true>
-                      : dev::render_kernel_lean<false, 6, true, false, false, true>;
+                      : dev::render_kernel_lean<false, FS_LEAN_WAVES, true, false, false, true>;
       ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, false>";
       if (ctx->has_textures) {  // textured scenes: the instantiation with texcoords + texel rows
         lk = count ? dev::render_kernel_lean<true, 6, true, false, true, true>
@@ -2951,7 +2955,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, false, false>";
       } else if (mode == KernelMode::kLeanSusp) {
         lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true, true>
-                   : dev::render_kernel_lean<false, 6, true, false, false, true, true>;
+                   : dev::render_kernel_lean<false, FS_LEAN_WAVES, true, false, false, true, true>;
         ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, true>";
       } else if (mode == KernelMode::kLeanBvh4) {  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
