@@ -2055,7 +2055,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       bool parked = false;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
-      const uint32_t nodes_before = tally.lane_nodes;
+      const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
       scene_trace_min<COUNT, WW, WIDE, TEX, SUSP>(S, r, h, stk, tally, pa, ovf, &ws, P.susp_thr, &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
@@ -2070,6 +2070,18 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         if (nv > 64) bin = 6;
         if (nv > 128) bin = 7;
         atomicAdd(&counters->phase[16 + bin], 1ull);
+        // bound for per-lane object sequencing: the wave's max over lanes of
+        // this call's node visits / leaf tests (vs node/leaf wave trips)
+        __shared__ uint32_t red[2];
+        const uint32_t nl = tally.lane_leaves - leaves_before;
+        const bool first = threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x);
+        if (first) red[0] = red[1] = 0;
+        atomicMax(&red[0], nv);
+        atomicMax(&red[1], nl);
+        if (first) {
+          atomicAdd(&counters->phase[24], (unsigned long long)red[0]);
+          atomicAdd(&counters->phase[25], (unsigned long long)red[1]);
+        }
       }
 #else
       PhaseAcc pa;
@@ -3031,6 +3043,8 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   std::fprintf(stderr, "[fs hist] node visits per segment: 0:%llu 1-4:%llu 5-8:%llu 9-16:%llu 17-32:%llu 33-64:%llu "
                "65-128:%llu >128:%llu\n", c.phase[16], c.phase[17], c.phase[18], c.phase[19], c.phase[20],
                c.phase[21], c.phase[22], c.phase[23]);
+  std::fprintf(stderr, "[fs seq] per-call wave max of lane node visits %llu (node trips %llu), of lane leaf tests "
+               "%llu (leaf trips %llu)\n", c.phase[24], c.phase[10], c.phase[25], c.phase[11]);
 #endif
   return FS_OK;
 }
