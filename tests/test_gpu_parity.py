@@ -344,14 +344,14 @@ def test_full_size_properties(scene_dir, gpu_renderer):
 
 
 def test_sample_groups_bit_exact(scene_dir, gpu_renderer, monkeypatch):
-    """A launch of G sample groups (G x 32 spp, folded in sample order by
-    fold_groups) gives the frame of G consecutive 32-spp launches, for any G,
+    """A launch of G sample groups (G x 64 spp, folded in sample order by
+    fold_groups) gives the frame of G consecutive 64-spp launches, for any G,
     with a ragged last chunk, on a tile shard, and matches the oracle."""
     r = gpu_renderer
     s = load_scene("c2", scene_dir)
     cam = s.camera(0)
     r.upload(s)
-    W, H, spp = 160, 72, 5 * 32 + 7  # 3x2 tiles of 64x64, ragged
+    W, H, spp = 160, 72, 5 * 64 + 7  # 3x2 tiles of 64x64; 5 full 64-spp chunks + a ragged one
     frames = {}
     for g in ("1", "2", "auto", "2-group-major"):
         monkeypatch.delenv("FS_GROUPS", raising=False)
@@ -363,9 +363,9 @@ def test_sample_groups_bit_exact(scene_dir, gpu_renderer, monkeypatch):
             r.render(cam, f, spp=spp, tile_offset=shard[0], tile_stride=shard[1])
             frames[g, shard] = ({p: f.read(p) for p in range(6)}, r.last_launches())
             f.close()
-    assert frames["1", (0, 1)][1] == (6, 32)
-    assert frames["2", (0, 1)][1] == (4, 64)     # groups 2+2+1, then the 7-spp chunk
-    assert frames["auto", (0, 1)][1] == (2, 160)  # a small frame takes all full chunks at once
+    assert frames["1", (0, 1)][1] == (6, 64)
+    assert frames["2", (0, 1)][1] == (4, 128)    # groups 2+2+1, then the 7-spp chunk
+    assert frames["auto", (0, 1)][1] == (2, 320)  # a small frame takes all full chunks at once
     for key, (planes, _) in frames.items():
         base = frames["1", key[1]][0]
         for p in range(6):
