@@ -19,8 +19,10 @@ constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS col
 #endif
 constexpr uint32_t kChunk = FS_CHUNK;  // samples per pixel per block (fs_render splits longer renders)
 // fs_render sizes sample groups so one launch holds at least this many blocks
-// (~21 per wave slot of 256 CUs x 24 waves).
-constexpr uint64_t kGroupTargetBlocks = 131072;
+// (~43 per wave slot of 256 CUs x 24 waves; C4 1080p x 1024 spp: 2 launches
+// of 512 spp, +2.6 % over 4 launches of 256 — a launch ends with a tail of
+// about one block's duration).
+constexpr uint64_t kGroupTargetBlocks = 262144;
 
 struct DevScene {
   const DevObject* __restrict__ objects;

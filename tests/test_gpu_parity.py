@@ -430,3 +430,26 @@ def test_error_paths(gpu_renderer):
     f.close()
     tiny.close()
     r.close()
+
+
+def test_rccl_gather_single_rank(scene_dir):
+    """The RCCL path of fs_frame_gather on a one-rank communicator (a GPU box
+    here has one device): pack_tiles + ncclGather run, the root's own tiles
+    stay as rendered, and misuse is reported."""
+    r = fsamd.Renderer(0)
+    s = load_scene("c1", scene_dir)
+    r.upload(s)
+    f = r.frame(100, 70)
+    p = r.render(s.camera(0), f, spp=2)
+    before = {pl: f.read(pl) for pl in range(6)}
+    with pytest.raises(RuntimeError):
+        r.gather(f, p)  # before fs_comm_init
+    r.comm_init(1, 0, fsamd.Renderer.comm_unique_id())
+    r.gather(f, p)
+    r.synchronize()
+    for pl in range(6):
+        np.testing.assert_array_equal(f.read(pl), before[pl])
+    with pytest.raises(RuntimeError):
+        r.gather(f, fsamd.render_params(100, 70, 2, tile_offset=0, tile_stride=2))  # tiling != ranks
+    f.close()
+    r.close()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes on the bench workload (reduced spp), one counter group per pass.
 set -o pipefail
-R=${1:-r01}; SPP=${2:-256}  # 256 spp = one launch of 4 sample groups of 64, the bench launch shape
+R=${1:-r01}; SPP=${2:-512}  # 512 spp = one launch of 8 sample groups of 64, the bench launch shape
 mkdir -p gpurun_out/$R/pmc
 export TMPDIR=/tmp
 CMD="python3 bench.py --steps 1 --warmup 0 --spp $SPP --no-cpu"
