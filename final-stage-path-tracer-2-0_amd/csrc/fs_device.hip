@@ -20,6 +20,11 @@
 #include "fs_scene.h"
 #include "fs_trace.h"
 
+// BVH-walk slab constants once per segment (1) or once per mesh walk (0, A/B)
+#ifndef FS_HOIST_SLOPES
+#define FS_HOIST_SLOPES 1
+#endif
+
 namespace fs {
 namespace dev {
 
@@ -1144,6 +1149,31 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
   }
 }
 
+// Per-ray slab constants of the BVH walks, computed once per segment. A
+// zero-length ray (a point test at the leaves) walks with a 1e-20 slope per
+// axis: every box that contains the start passes the slab test (entry <= 0 <=
+// exit), so the cull stays a superset of the point-in-box test without a
+// per-node branch. v_rcp (about 1 ulp) instead of IEEE division: the slab
+// test is a conservative cull whose t margins (1e-6 absolute, 2e-6 relative)
+// and box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
+struct Slopes {
+  float ix, iy, iz, ox, oy, oz;
+};
+__device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) {
+  const float tiny = 1e-20f;
+  float dx = fabsf(r.dir.x) < tiny || zl ? copysignf(tiny, r.dir.x) : r.dir.x;
+  float dy = fabsf(r.dir.y) < tiny || zl ? copysignf(tiny, r.dir.y) : r.dir.y;
+  float dz = fabsf(r.dir.z) < tiny || zl ? copysignf(tiny, r.dir.z) : r.dir.z;
+  Slopes sl;
+  sl.ix = __builtin_amdgcn_rcpf(dx);
+  sl.iy = __builtin_amdgcn_rcpf(dy);
+  sl.iz = __builtin_amdgcn_rcpf(dz);
+  sl.ox = -r.start.x * sl.ix;
+  sl.oy = -r.start.y * sl.iy;
+  sl.oz = -r.start.z * sl.iz;
+  return sl;
+}
+
 // SUSP: when at most `thr` lanes are still walking while other live lanes of
 // the wave wait, the walkers park (state to *ws) and return true; the wave
 // moves on and they resume from *ws in a later iteration (same operations in
@@ -1152,22 +1182,11 @@ template <bool COUNT, bool SUSP = false, int ZLMODE = -1>  // ZLMODE as in test_
 __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl_rt,
                                             MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                             WalkSuspend* ws = nullptr, bool resume = false, uint32_t thr = 0,
-                                            uint32_t live = 0) {
+                                            uint32_t live = 0, const Slopes* pre = nullptr) {
   const bool zl = ZLMODE < 0 ? zl_rt : ZLMODE == 1;
   constexpr uint32_t kNone = 0x7FFFFFFFu;  // empty-stack sentinel (no leaf bit, never a node index)
-  const float tiny = 1e-20f;
-  // A zero-length ray (a point test at the leaves) walks with a 1e-20 slope
-  // per axis: every box that contains the start passes the slab test (entry
-  // <= 0 <= exit), so the cull stays a superset of the point-in-box test
-  // without a per-node branch.
-  float dx = fabsf(r.dir.x) < tiny || zl ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny || zl ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny || zl ? copysignf(tiny, r.dir.z) : r.dir.z;
-  // v_rcp (about 1 ulp) instead of IEEE division: the slab test is a
-  // conservative cull whose t margins (1e-6 absolute, 2e-6 relative) and
-  // box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
-  float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
-  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
+  const Slopes sl = pre ? *pre : walk_slopes(r, zl);
+  const float ix = sl.ix, iy = sl.iy, iz = sl.iz, ox = sl.ox, oy = sl.oy, oz = sl.oz;
   uint32_t w = root, leaf = 0, sp = 0;
   if (SUSP && resume) {
     w = ws->w;
@@ -1403,6 +1422,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   bool zl = zero_len(r);
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
   bool park = false;
+#if FS_HOIST_SLOPES
+  const Slopes sl = walk_slopes(r, zl);  // once per segment, not once per mesh walk
+  const Slopes* slp = &sl;
+#else
+  const Slopes* slp = nullptr;
+#endif
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
     if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
@@ -1420,14 +1445,14 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         // branch out of the loop, measured 3-4 % slower: code size)
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
-                                          o->i5 ? susp_thr : 0u, live);
+                                          o->i5 ? susp_thr : 0u, live, slp);
         if (resume_here) resuming = false;
         if (park) continue;
       } else if (visit) {
         if (WIDE && o->i3 >= 0)
           traverse4_ww<COUNT>(S, (uint32_t)o->i3, (int32_t)oi, r, zl, h, LaneStack{stk, ovf}, tally);
         else if (WW)
-          traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+          traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
         else
           traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
       }
