@@ -453,3 +453,30 @@ def test_rccl_gather_single_rank(scene_dir):
         r.gather(f, fsamd.render_params(100, 70, 2, tile_offset=0, tile_stride=2))  # tiling != ranks
     f.close()
     r.close()
+
+
+def test_c4_eight_rank_shards_equal_single_gpu(scene_dir, gpu_renderer):
+    """The bench workload's 8-GPU partition, on one device: the union of the
+    eight tile shards (each rendered as its own sample-group launches) is the
+    1-GPU frame bit for bit, at 1080p on the 1 M-triangle scene."""
+    r = gpu_renderer
+    s = load_scene("c4", scene_dir)
+    cam = s.camera(0)
+    r.upload(s)
+    W, H, spp = 1920, 1080, 128
+    full = r.frame(W, H)
+    r.render(cam, full, spp=spp)
+    ref = {p: full.read(p) for p in (fsamd.PLANE_COLOR, fsamd.PLANE_COUNT, fsamd.PLANE_MATERIAL)}
+    assert (ref[fsamd.PLANE_COUNT] == spp).all()
+    part = r.frame(W, H)
+    got = {p: np.zeros_like(v) for p, v in ref.items()}
+    for k in range(8):
+        part.reset()
+        r.render(cam, part, spp=spp, tile_offset=k, tile_stride=8)
+        own = part.read(fsamd.PLANE_COUNT) > 0
+        for p in got:
+            got[p][own] = part.read(p)[own]
+    for p in got:
+        np.testing.assert_array_equal(got[p], ref[p], err_msg=f"plane {p}")
+    full.close()
+    part.close()
