@@ -20,6 +20,12 @@
 #include "fs_scene.h"
 #include "fs_trace.h"
 
+// Wave priority inside BVH walks (s_setprio): waves in a walk issue first,
+// so the dependent node fetches of the latency-bound walks start sooner
+// (C2 +1.3 %, C3 +0.8 %, C4 neutral; 1 and 3 measure the same; 0 = off)
+#ifndef FS_TRAV_PRIO
+#define FS_TRAV_PRIO 1
+#endif
 // BVH-walk slab constants once per segment (1) or once per mesh walk (0, A/B)
 #ifndef FS_HOIST_SLOPES
 #define FS_HOIST_SLOPES 1
@@ -1196,6 +1202,9 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;  // h.t only changes in the leaf tests
   uint32_t trips = 0;
   bool susp = false;
+#if FS_TRAV_PRIO
+  __builtin_amdgcn_s_setprio(FS_TRAV_PRIO);
+#endif
   while ((w != kNone || leaf) && !(SUSP && susp)) {
     while (!(w & kLeafBit) && w != kNone) {
       const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
@@ -1262,6 +1271,9 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
     }
     tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
   }
+#if FS_TRAV_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   if (SUSP && susp) {
     ws->oi = oi;
     ws->w = w;
