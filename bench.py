@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scene-dir", default=None)
+    ap.add_argument("--bvh", default="device", choices=["device", "host"],
+                    help="BVH builder of large meshes (fs_upload_scene_ex FS_UPLOAD_GPU_BVH, or host SAH)")
     return ap.parse_args()
 
 
@@ -88,7 +90,7 @@ def main():
     cam = scene.camera(0)
     gen_s = time.time() - t0
     r = fsamd.Renderer(local_rank)
-    r.upload(scene)
+    r.upload(scene, gpu_bvh=args.bvh == "device")
     stats = r.scene_stats()
     log(f"rank {rank}: scene {args.scene} written+loaded in {gen_s:.1f}s, BVH {stats}")
     W, H, spp = args.width, args.height, args.spp
@@ -181,7 +183,7 @@ def main():
             "data": "synthetic (seeded procedural scene, per-(pixel,sample) seeded xorshift64*)",
             "config": {"workload": WORKLOADS[args.scene], "scene": args.scene, "width": W, "height": H,
                        "spp": spp, "triangles": stats["triangles"], "bvh_nodes": stats["nodes"],
-                       "bvh_build_ms": round(stats["build_ms"], 1),
+                       "bvh_build_ms": round(stats["build_ms"], 1), "bvh_builder": args.bvh,
                        "parallelism": f"64x64 tiles round-robin over {world} GPU(s)"
                                       + (" + RCCL ncclGather to rank 0" if world > 1 else "")},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -16,6 +16,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "fs_bvh_gpu.h"
 #include "fs_kernels.h"
 #include "fs_scene.h"
 #include "fs_trace.h"
@@ -2453,6 +2454,8 @@ struct fs_context {
   uint32_t num_objects = 0;
   PreparedScene host;
   double upload_ms = 0.0;
+  double gpu_bvh_ms = 0.0;                              // device BVH builds of the last upload
+  uint64_t gpu_bvh_nodes = 0, gpu_bvh_reserved = 0;     // nodes they used / reserved
   float last_ms = 0.0f;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -2707,10 +2710,26 @@ int fs_destroy(fs_context* ctx) {
 }
 
 int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
+  const char* e = std::getenv("FS_GPU_BVH");
+  return fs_upload_scene_ex(ctx, desc, (e && std::atoi(e)) ? FS_UPLOAD_GPU_BVH : 0u);
+}
+
+int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flags) {
   if (!ctx) return fail(FS_ERR_INVALID, "null context");
+  if (flags & ~FS_UPLOAD_GPU_BVH) return fail(FS_ERR_INVALID, "unknown upload flags");
   std::string err;
   PreparedScene P;
-  int rc = prepare_scene(desc, &P, &err);
+  // Meshes this large take the device build (fs_bvh_gpu.hip); smaller ones
+  // stay on the host, where a tree of a few thousand faces is cheaper to
+  // build than the level-synchronous launches. FS_GPU_BVH_MIN_TRIS lowers
+  // the threshold (tests), never below the device builder's minimum.
+  uint32_t gpu_min = 0;
+  if (flags & FS_UPLOAD_GPU_BVH) {
+    const char* m = std::getenv("FS_GPU_BVH_MIN_TRIS");
+    gpu_min = m ? (uint32_t)std::strtoul(m, nullptr, 10) : kGpuBvhMinTris;
+    gpu_min = std::max(gpu_min, kGpuBvhFloor);
+  }
+  int rc = prepare_scene(desc, &P, &err, gpu_min);
   if (rc) return fail(rc, err);
   if (P.materials.size() > 255) return fail(FS_ERR_INVALID, "at most 255 materials are supported");
   if ((rc = set_device(ctx))) return rc;
@@ -2728,6 +2747,32 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
   if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
   ctx->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ctx->gpu_bvh_ms = 0.0;
+  ctx->gpu_bvh_nodes = ctx->gpu_bvh_reserved = 0;
+  for (DeferredMesh& D : P.deferred) {  // device BVH builds into the reserved blocks
+    GpuBvhJob job{};
+    job.lo = D.lo.data();
+    job.hi = D.hi.data();
+    job.tris = D.tris.data();
+    job.normals = D.normals.empty() ? nullptr : D.normals.data();
+    job.tex = D.tex.empty() ? nullptr : D.tex.data();
+    job.num_tris = D.num_tris;
+    job.leaf = bvh_leaf_target();
+    job.node_base = D.node_base;
+    job.tri_base = D.tri_base;
+    GpuBvhResult res;
+    rc = gpu_build_mesh_bvh(ctx->stream, job, (BvhNode*)ctx->nodes.p, (DevTri*)ctx->tris.p, (float*)ctx->tri_normals.p,
+                            (float*)ctx->tri_tex.p, &res, &err);
+    if (rc) return fail(rc, "mesh " + std::to_string(D.mesh) + ": " + err);
+    P.max_depth = std::max(P.max_depth, res.max_depth);
+    ctx->gpu_bvh_ms += res.build_ms;
+    ctx->gpu_bvh_nodes += res.nodes_used;
+    ctx->gpu_bvh_reserved += D.num_tris;
+    if (std::getenv("FS_BUILD_LOG"))
+      std::fprintf(stderr, "[fs build] mesh %u: %u tris, device bvh %.1f ms (%u levels, %u nodes, depth %u)\n", D.mesh,
+                   D.num_tris, res.build_ms, res.levels, res.nodes_used, res.max_depth);
+    D = DeferredMesh();  // release the host copies
+  }
   DevScene& S = ctx->scene;
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
@@ -2768,10 +2813,10 @@ int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms, uint64_
                    uint64_t* num_nodes, uint64_t* device_bytes) {
   if (!ctx) return fail(FS_ERR_INVALID, "null context");
   if (!ctx->have_scene) return fail(FS_ERR_STATE, "no scene uploaded");
-  if (build_ms) *build_ms = ctx->host.build_ms;
+  if (build_ms) *build_ms = ctx->host.build_ms + ctx->gpu_bvh_ms;
   if (upload_ms) *upload_ms = ctx->upload_ms;
   if (num_triangles) *num_triangles = ctx->host.tris.size();
-  if (num_nodes) *num_nodes = ctx->host.nodes.size();
+  if (num_nodes) *num_nodes = ctx->host.nodes.size() - ctx->gpu_bvh_reserved + ctx->gpu_bvh_nodes;
   if (device_bytes)
     *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->nodes4.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
                      ctx->materials.bytes + ctx->table.bytes;

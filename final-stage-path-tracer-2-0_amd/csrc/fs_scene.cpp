@@ -630,7 +630,9 @@ int build_object(const fs_object& o, DevObject* out, std::string* err) {
 
 }  // namespace
 
-int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) {
+uint32_t bvh_leaf_target() { return leaf_target_env(); }
+
+int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, uint32_t gpu_bvh_min_tris) {
   auto t0 = std::chrono::steady_clock::now();
   if (!d || !out) {
     *err = "null scene";
@@ -705,9 +707,19 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
   std::vector<MeshOut> mesh_out(d->num_meshes);
   const bool use4 = bvh4_enabled();
   bool any_normals = false, any_tex = false;
+  size_t all_tris = 0;
   for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
     if (d->meshes[mi].normals && d->meshes[mi].num_normals) any_normals = true;
     if (d->meshes[mi].texcoords && d->meshes[mi].num_texcoords) any_tex = true;
+    all_tris += d->meshes[mi].num_triangles;
+  }
+  // A BVH2 over n faces has at most n-1 inner nodes: size the arrays once
+  // (regrowing a 1 M-face scene's arrays costs tens of ms of copies).
+  if (all_tris <= kMaxTriangles) {
+    S.nodes.reserve(all_tris + d->num_meshes);
+    S.tris.reserve(all_tris);
+    if (any_normals) S.tri_normals.reserve(12 * all_tris);
+    if (any_tex) S.tri_tex.reserve(6 * all_tris);
   }
   for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
     const fs_mesh& m = d->meshes[mi];
@@ -802,6 +814,41 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       *err = "too many triangles for the 24-bit leaf encoding";
       return FS_ERR_INVALID;
     }
+    for (DevTri& t : mtris) t.mesh_obj = mi;
+    if (gpu_bvh_min_tris && m.num_triangles >= gpu_bvh_min_tris) {
+      // Deferred to the device build: reserve the node block (a binary tree
+      // over n faces has at most n-1 inner nodes) and the triangle slots.
+      DeferredMesh D;
+      D.mesh = mi;
+      D.num_tris = m.num_triangles;
+      D.node_base = (uint32_t)S.nodes.size();
+      D.tri_base = (uint32_t)S.tris.size();
+      D.lo.resize(3 * (size_t)m.num_triangles);
+      D.hi.resize(3 * (size_t)m.num_triangles);
+      for (uint32_t f = 0; f < m.num_triangles; f++) {
+        Box b;
+        for (int k = 0; k < 3; k++) b.grow(&corner_pos[9 * (size_t)f + 3 * k]);
+        for (int k = 0; k < 3; k++) {
+          D.lo[3 * (size_t)f + k] = b.lo[k];
+          D.hi[3 * (size_t)f + k] = b.hi[k];
+        }
+      }
+      BvhNode zero;
+      std::memset(&zero, 0, sizeof(zero));
+      S.nodes.resize(S.nodes.size() + m.num_triangles, zero);
+      DevTri tz;
+      std::memset(&tz, 0, sizeof(tz));
+      S.tris.resize(S.tris.size() + m.num_triangles, tz);
+      if (any_normals) S.tri_normals.resize(S.tri_normals.size() + 12 * (size_t)m.num_triangles, 0.0f);
+      if (any_tex) S.tri_tex.resize(S.tri_tex.size() + 6 * (size_t)m.num_triangles, 0.0f);
+      D.tris = std::move(mtris);
+      if (any_normals) D.normals = std::move(mnormals);
+      if (any_tex) D.tex = std::move(mtex);
+      mesh_out[mi].root = D.node_base;
+      mesh_out[mi].root4 = -1;
+      S.deferred.push_back(std::move(D));
+      continue;
+    }
     auto tp = std::chrono::steady_clock::now();
     std::vector<Prim> prims(m.num_triangles);
     for (uint32_t f = 0; f < m.num_triangles; f++) {
@@ -812,7 +859,6 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err) 
       for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
       p.face = f;
     }
-    for (DevTri& t : mtris) t.mesh_obj = mi;
     BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex);
     auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);

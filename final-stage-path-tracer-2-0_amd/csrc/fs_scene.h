@@ -93,6 +93,17 @@ struct DevTri {
 };
 static_assert(sizeof(DevTri) == 80, "DevTri layout");
 
+// A mesh whose BVH is built on the device (fs_upload_scene_ex with
+// FS_UPLOAD_GPU_BVH, fs_bvh_gpu.hip). prepare_scene reserves num_tris nodes
+// from node_base and num_tris triangle slots (plus normal/texcoord slots)
+// from tri_base in the scene arrays, and keeps the face-order inputs here.
+struct DeferredMesh {
+  uint32_t mesh = 0, num_tris = 0, node_base = 0, tri_base = 0;
+  std::vector<float> lo, hi;  // 3 floats per face: the primitive box
+  std::vector<DevTri> tris;   // face order
+  std::vector<float> normals, tex;  // face order, or empty
+};
+
 struct PreparedScene {
   std::vector<DevObject> objects;
   std::vector<BvhNode> nodes;
@@ -107,10 +118,16 @@ struct PreparedScene {
   int32_t sky = 0;
   uint32_t max_depth = 0;
   double build_ms = 0.0;
+  std::vector<DeferredMesh> deferred;  // meshes left for the device build
 };
 
 // Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
 // one SAH BVH per mesh. Returns FS_OK or an fs_status with *err set.
-int prepare_scene(const fs_scene_desc* desc, PreparedScene* out, std::string* err);
+// Meshes of at least gpu_bvh_min_tris triangles (0: none) are not built
+// here but deferred to the device build (PreparedScene::deferred).
+int prepare_scene(const fs_scene_desc* desc, PreparedScene* out, std::string* err, uint32_t gpu_bvh_min_tris = 0);
+
+// The leaf-size target both builders use (FS_BVH_LEAF overrides, default 2).
+uint32_t bvh_leaf_target();
 
 }  // namespace fs

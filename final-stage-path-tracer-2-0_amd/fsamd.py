@@ -87,6 +87,8 @@ class fs_counters(C.Structure):
                 ("tri_tests", C.c_uint64), ("prim_tests", C.c_uint64)]
 
 
+UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
+
 # Exported symbols of include/fs_trace.h, with their ctypes signatures.
 _VP = C.c_void_p
 GPU_SYMBOLS = {
@@ -96,6 +98,7 @@ GPU_SYMBOLS = {
     "fs_create": ([C.c_int, C.POINTER(_VP)], C.c_int),
     "fs_destroy": ([_VP], C.c_int),
     "fs_upload_scene": ([_VP, _VP], C.c_int),
+    "fs_upload_scene_ex": ([_VP, _VP, C.c_uint32], C.c_int),
     "fs_scene_stats": ([_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], C.c_int),
     "fs_frame_create": ([_VP, C.c_uint32, C.c_uint32, C.POINTER(_VP)], C.c_int),
@@ -342,10 +345,16 @@ class Renderer:
         self.ctx = h
         self._scene_ref = None
 
-    def upload(self, scene):
-        """scene: HostScene, or a ctypes pointer/void* to an fs_scene_desc."""
+    def upload(self, scene, gpu_bvh=None):
+        """scene: HostScene, or a ctypes pointer/void* to an fs_scene_desc.
+        gpu_bvh: True/False selects the device/host BVH build of large meshes
+        (fs_upload_scene_ex); None keeps fs_upload_scene (FS_GPU_BVH env)."""
         ptr = scene.desc_ptr() if isinstance(scene, HostScene) else scene
-        _check(gpu_lib().fs_upload_scene(self.ctx, ptr), "fs_upload_scene")
+        if gpu_bvh is None:
+            _check(gpu_lib().fs_upload_scene(self.ctx, ptr), "fs_upload_scene")
+        else:
+            flags = UPLOAD_GPU_BVH if gpu_bvh else 0
+            _check(gpu_lib().fs_upload_scene_ex(self.ctx, ptr, flags), "fs_upload_scene_ex")
         self._scene_ref = scene
 
     def scene_stats(self):

@@ -214,7 +214,15 @@ int fs_destroy(fs_context* ctx);
 /* Copies the scene, builds per-mesh BVHs on the host and uploads SoA arrays.
  * Replaces any scene previously uploaded to ctx. */
 int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc);
-/* Host BVH build + upload time of the last fs_upload_scene, in ms. */
+/* fs_upload_scene with options. FS_UPLOAD_GPU_BVH builds the BVH of every
+ * mesh of >= 65536 triangles on the device (binned SAH, same tree rules as
+ * the host build; the frames are identical). fs_upload_scene
+ * behaves as flags = 0 unless the environment sets FS_GPU_BVH=1. Replaces
+ * the reference's load-time octree build, mesh.cpp:117-152. */
+#define FS_UPLOAD_GPU_BVH 1u
+int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flags);
+/* Scene build (host preparation + any device BVH build) and upload time of
+ * the last upload, in ms. */
 int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms,
                    uint64_t* num_triangles, uint64_t* num_nodes,
                    uint64_t* device_bytes);

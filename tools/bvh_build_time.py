@@ -1,0 +1,48 @@
+"""Scene build time, host vs device BVH (fs_upload_scene_ex), per scene.
+
+  python tools/bvh_build_time.py [--scenes c3,c4] [--reps 3]
+
+Prints one JSON line per (scene, builder) with the median build_ms of
+fs_scene_stats (host preparation + device BVH build) and the node count.
+Set FS_BUILD_LOG=1 for the per-phase split of the device build.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "final-stage-path-tracer-2-0_amd"))
+import fsamd  # noqa: E402
+import scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scenes", default="c3,c4")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    d = tempfile.mkdtemp(prefix="fs_bvht_")
+    r = fsamd.Renderer(0)
+    for name in a.scenes.split(","):
+        path = scenes.write(name, os.path.join(d, name))
+        fsamd.reset_main_rng()
+        s = fsamd.HostScene.load(path)
+        fsamd.initialize_materials()
+        for gpu in (False, True):
+            runs = []
+            for _ in range(a.reps + 1):  # first upload warms the allocator and code objects
+                r.upload(s, gpu_bvh=gpu)
+                runs.append(r.scene_stats())
+            runs = runs[1:]
+            print(json.dumps({"scene": name, "builder": "device" if gpu else "host",
+                              "build_ms": round(statistics.median(x["build_ms"] for x in runs), 1),
+                              "upload_ms": round(statistics.median(x["upload_ms"] for x in runs), 1),
+                              "nodes": runs[-1]["nodes"], "triangles": runs[-1]["triangles"]}), flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
