@@ -1002,9 +1002,13 @@ bool ensure_scene(Engine& e, Scene* scene) {
       std::fprintf(stderr, "[fs] %s\n", err.c_str());
       return false;
     }
-    int rc = fs_upload_scene(e.ctx, d);
+    // Large meshes get their BVH built on the device (same frames, about a
+    // tenth of the host build time); FS_GPU_BVH=0 keeps the host build.
+    const char* gb = std::getenv("FS_GPU_BVH");
+    const uint32_t flags = (gb && std::strcmp(gb, "0") == 0) ? 0u : FS_UPLOAD_GPU_BVH;
+    int rc = fs_upload_scene_ex(e.ctx, d, flags);
     if (rc) {
-      engine_fail(e, rc, "fs_upload_scene");
+      engine_fail(e, rc, "fs_upload_scene_ex");
       return false;
     }
     e.scene = scene;

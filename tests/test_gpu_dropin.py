@@ -14,15 +14,16 @@ from conftest import ROOT, load_scene
 pytestmark = pytest.mark.gpu
 
 
-def test_trace_scene_loop_matches_oracle(scene_dir, tmp_path):
+@pytest.mark.parametrize("name,W,H,N", [("c2", 64, 40, 6), ("c4", 48, 32, 3)])
+def test_trace_scene_loop_matches_oracle(name, W, H, N, scene_dir, tmp_path):
+    """C4's 1 M-face mesh takes the device BVH build inside TraceScene."""
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], check=True)
-    path = scenes.write("c2", os.path.join(scene_dir, "c2_dropin"))
-    W, H, N = 64, 40, 6
+    path = scenes.write(name, os.path.join(scene_dir, f"{name}_dropin"))
     ppm, f32 = str(tmp_path / "out.ppm"), str(tmp_path / "out.f32")
     subprocess.run([os.path.join(ROOT, "examples", "trace_scene"), path, str(W), str(H), str(N), ppm, f32],
                    check=True, timeout=300)
     color = np.fromfile(f32, np.float32).reshape(H, W, 3)
-    s = load_scene("c2", scene_dir)
+    s = load_scene(name, scene_dir)
     ref = oracle_py.Scene(s.desc_ptr()).render(s.camera(0), fsamd.render_params(W, H, N), threads=8)
     np.testing.assert_array_equal(color, ref.color)
     raw = open(ppm, "rb").read()

@@ -480,3 +480,34 @@ def test_c4_eight_rank_shards_equal_single_gpu(scene_dir, gpu_renderer):
         np.testing.assert_array_equal(got[p], ref[p], err_msg=f"plane {p}")
     full.close()
     part.close()
+
+
+def test_c5_2160p_shards_equal_single_gpu(scene_dir, gpu_renderer):
+    """BASELINE configs[4] shape (C5: the C4 scene at 3840x2160, tiles over 8
+    GPUs) at 64 spp on one device: one launch of 129 600 blocks, every pixel
+    gets its samples, and the eight shards' union is the 1-GPU frame bit for
+    bit."""
+    r = gpu_renderer
+    s = load_scene("c4", scene_dir)
+    cam = s.camera(0)
+    r.upload(s, gpu_bvh=True)
+    W, H, spp = 3840, 2160, 64
+    full = r.frame(W, H)
+    r.render(cam, full, spp=spp)
+    launches, launch_spp = r.last_launches()
+    assert launches == 1 and launch_spp == spp, (launches, launch_spp)
+    ref = {p: full.read(p) for p in (fsamd.PLANE_COLOR, fsamd.PLANE_COUNT, fsamd.PLANE_MATERIAL)}
+    assert (ref[fsamd.PLANE_COUNT] == spp).all()
+    assert np.isfinite(ref[fsamd.PLANE_COLOR]).all()
+    part = r.frame(W, H)
+    got = {p: np.zeros_like(v) for p, v in ref.items()}
+    for k in range(8):
+        part.reset()
+        r.render(cam, part, spp=spp, tile_offset=k, tile_stride=8)
+        own = part.read(fsamd.PLANE_COUNT) > 0
+        for p in got:
+            got[p][own] = part.read(p)[own]
+    for p in got:
+        np.testing.assert_array_equal(got[p], ref[p], err_msg=f"plane {p}")
+    full.close()
+    part.close()
