@@ -630,6 +630,24 @@ int build_object(const fs_object& o, DevObject* out, std::string* err) {
 
 }  // namespace
 
+// Per-face preparation of large meshes runs on up to kPrepThreads threads
+// (each face's record depends only on that face).
+constexpr uint32_t kPrepThreads = 16;
+constexpr uint32_t kPrepParallelMin = 1u << 16;
+template <class F>
+void parallel_chunks(uint32_t n, F&& fn) {
+  uint32_t t = std::min<uint32_t>(kPrepThreads, std::max(1u, std::thread::hardware_concurrency()));
+  if (n < kPrepParallelMin) t = 1;
+  const uint32_t per = (n + t - 1) / t;
+  std::vector<std::thread> pool;
+  for (uint32_t c = 1; c < t; c++) {
+    const uint32_t b = std::min(n, c * per), e = std::min(n, b + per);
+    if (b < e) pool.emplace_back(fn, c, b, e);
+  }
+  fn(0u, 0u, std::min(n, per));
+  for (std::thread& th : pool) th.join();
+}
+
 uint32_t bvh_leaf_target() { return leaf_target_env(); }
 
 int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, uint32_t gpu_bvh_min_tris) {
@@ -769,25 +787,26 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     std::vector<float> mnormals, mtex;
     if (any_normals) mnormals.assign(12 * (size_t)m.num_triangles, 0.0f);
     if (any_tex) mtex.assign(6 * (size_t)m.num_triangles, 0.0f);
-    for (uint32_t f = 0; f < m.num_triangles; f++) {
+    // Faces are independent: large meshes fill their records on several
+    // threads. The first bad face (lowest index) is reported, as the
+    // sequential loop would.
+    std::vector<uint64_t> bad(kPrepThreads, ~0ull);  // per chunk: (face << 2) | kind of the first bad face
+    auto fill_faces = [&](uint32_t chunk, uint32_t f0, uint32_t f1) {
+    for (uint32_t f = f0; f < f1; f++) {
       const int32_t* c = m.corners + 9 * (size_t)f;
       uint32_t vi[3], ni[3], ti[3];
+      uint32_t kind = 0;
       for (int k = 0; k < 3; k++) {  // winding reversed (mesh.cpp:250-260)
         vi[k] = (uint32_t)c[3 * (2 - k) + 0];
         ni[k] = (uint32_t)c[3 * (2 - k) + 1];
         ti[k] = (uint32_t)c[3 * (2 - k) + 2];
-        if (vi[k] >= m.num_positions) {
-          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": vertex index out of range";
-          return FS_ERR_INVALID;
-        }
-        if (nn && ni[k] >= nn) {  // normals_.at() would throw (mesh.cpp:292)
-          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": normal index out of range";
-          return FS_ERR_INVALID;
-        }
-        if (nt && ti[k] >= nt) {
-          *err = "mesh " + std::to_string(mi) + " face " + std::to_string(f) + ": texcoord index out of range";
-          return FS_ERR_INVALID;
-        }
+        if (!kind && vi[k] >= m.num_positions) kind = 1;
+        if (!kind && nn && ni[k] >= nn) kind = 2;  // normals_.at() would throw (mesh.cpp:292)
+        if (!kind && nt && ti[k] >= nt) kind = 3;
+      }
+      if (kind) {
+        bad[chunk] = ((uint64_t)f << 2) | kind;
+        return;
       }
       DevTri& t = mtris[f];
       std::memset(&t, 0, sizeof(t));
@@ -807,6 +826,15 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
           mtex[6 * (size_t)f + 2 * k + 1] = m.texcoords[2 * (size_t)ti[k] + 1];
         }
     }
+    };
+    parallel_chunks(m.num_triangles, fill_faces);
+    const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
+    if (first_bad != ~0ull) {
+      static const char* what[4] = {"", "vertex", "normal", "texcoord"};
+      *err = "mesh " + std::to_string(mi) + " face " + std::to_string(first_bad >> 2) + ": " + what[first_bad & 3u] +
+             " index out of range";
+      return FS_ERR_INVALID;
+    }
     mesh_out[mi].texcoords = nt > 0;
     mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
     if (!mesh_out[mi].tree) continue;
@@ -825,14 +853,16 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.tri_base = (uint32_t)S.tris.size();
       D.lo.resize(3 * (size_t)m.num_triangles);
       D.hi.resize(3 * (size_t)m.num_triangles);
-      for (uint32_t f = 0; f < m.num_triangles; f++) {
-        Box b;
-        for (int k = 0; k < 3; k++) b.grow(&corner_pos[9 * (size_t)f + 3 * k]);
-        for (int k = 0; k < 3; k++) {
-          D.lo[3 * (size_t)f + k] = b.lo[k];
-          D.hi[3 * (size_t)f + k] = b.hi[k];
+      parallel_chunks(m.num_triangles, [&](uint32_t, uint32_t f0, uint32_t f1) {
+        for (uint32_t f = f0; f < f1; f++) {
+          Box b;
+          for (int k = 0; k < 3; k++) b.grow(&corner_pos[9 * (size_t)f + 3 * k]);
+          for (int k = 0; k < 3; k++) {
+            D.lo[3 * (size_t)f + k] = b.lo[k];
+            D.hi[3 * (size_t)f + k] = b.hi[k];
+          }
         }
-      }
+      });
       BvhNode zero;
       std::memset(&zero, 0, sizeof(zero));
       S.nodes.resize(S.nodes.size() + m.num_triangles, zero);
