@@ -2455,7 +2455,7 @@ struct fs_context {
   PreparedScene host;
   double upload_ms = 0.0;
   double gpu_bvh_ms = 0.0;                              // device BVH builds of the last upload
-  uint64_t gpu_bvh_nodes = 0, gpu_bvh_reserved = 0;     // nodes they used / reserved
+  uint64_t gpu_bvh_nodes = 0, gpu_bvh_tris = 0;         // nodes they built / triangles they placed
   float last_ms = 0.0f;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -2477,9 +2477,11 @@ int set_device(fs_context* ctx) {
   return FS_OK;
 }
 
-int upload(fs_context* ctx, DevBuf* b, const void* src, size_t bytes) {
+// Allocates bytes + extra (the extra tail is left for device-side writers)
+// and copies `bytes` from the host.
+int upload(fs_context* ctx, DevBuf* b, const void* src, size_t bytes, size_t extra = 0) {
   b->release();
-  size_t alloc = bytes ? bytes : 16;
+  size_t alloc = bytes + extra ? bytes + extra : 16;
   FS_HIP(hipMalloc(&b->p, alloc));
   b->bytes = alloc;
   if (bytes) FS_HIP(hipMemcpyAsync(b->p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -2736,11 +2738,19 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   auto t0 = std::chrono::steady_clock::now();
   ctx->have_scene = false;
   if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
-  if ((rc = upload(ctx, &ctx->nodes, P.nodes.data(), P.nodes.size() * sizeof(BvhNode)))) return rc;
+  if ((rc = upload(ctx, &ctx->nodes, P.nodes.data(), P.nodes.size() * sizeof(BvhNode),
+                   (size_t)P.deferred_nodes * sizeof(BvhNode))))
+    return rc;
   if ((rc = upload(ctx, &ctx->nodes4, P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node)))) return rc;
-  if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri)))) return rc;
-  if ((rc = upload(ctx, &ctx->tri_normals, P.tri_normals.data(), P.tri_normals.size() * sizeof(float)))) return rc;
-  if ((rc = upload(ctx, &ctx->tri_tex, P.tri_tex.data(), P.tri_tex.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri),
+                   (size_t)P.deferred_tris * sizeof(DevTri))))
+    return rc;
+  if ((rc = upload(ctx, &ctx->tri_normals, P.tri_normals.data(), P.tri_normals.size() * sizeof(float),
+                   P.any_normals ? 48ull * P.deferred_tris : 0)))
+    return rc;
+  if ((rc = upload(ctx, &ctx->tri_tex, P.tri_tex.data(), P.tri_tex.size() * sizeof(float),
+                   P.any_tex ? 24ull * P.deferred_tris : 0)))
+    return rc;
   if ((rc = upload(ctx, &ctx->tex_rgb, P.tex_rgb.data(), P.tex_rgb.size() * sizeof(float)))) return rc;
   if ((rc = upload(ctx, &ctx->tex_info, P.tex_info.data(), P.tex_info.size() * sizeof(uint32_t)))) return rc;
   if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
@@ -2748,7 +2758,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   FS_HIP(hipStreamSynchronize(ctx->stream));
   ctx->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   ctx->gpu_bvh_ms = 0.0;
-  ctx->gpu_bvh_nodes = ctx->gpu_bvh_reserved = 0;
+  ctx->gpu_bvh_nodes = 0;
+  ctx->gpu_bvh_tris = P.deferred_tris;
   for (DeferredMesh& D : P.deferred) {  // device BVH builds into the reserved blocks
     GpuBvhJob job{};
     job.lo = D.lo.data();
@@ -2767,7 +2778,6 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
     P.max_depth = std::max(P.max_depth, res.max_depth);
     ctx->gpu_bvh_ms += res.build_ms;
     ctx->gpu_bvh_nodes += res.nodes_used;
-    ctx->gpu_bvh_reserved += D.num_tris;
     if (std::getenv("FS_BUILD_LOG"))
       std::fprintf(stderr, "[fs build] mesh %u: %u tris, device bvh %.1f ms (%u levels, %u nodes, depth %u)\n", D.mesh,
                    D.num_tris, res.build_ms, res.levels, res.nodes_used, res.max_depth);
@@ -2815,8 +2825,8 @@ int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms, uint64_
   if (!ctx->have_scene) return fail(FS_ERR_STATE, "no scene uploaded");
   if (build_ms) *build_ms = ctx->host.build_ms + ctx->gpu_bvh_ms;
   if (upload_ms) *upload_ms = ctx->upload_ms;
-  if (num_triangles) *num_triangles = ctx->host.tris.size();
-  if (num_nodes) *num_nodes = ctx->host.nodes.size() - ctx->gpu_bvh_reserved + ctx->gpu_bvh_nodes;
+  if (num_triangles) *num_triangles = ctx->host.tris.size() + ctx->gpu_bvh_tris;
+  if (num_nodes) *num_nodes = ctx->host.nodes.size() + ctx->gpu_bvh_nodes;
   if (device_bytes)
     *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->nodes4.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
                      ctx->materials.bytes + ctx->table.bytes;

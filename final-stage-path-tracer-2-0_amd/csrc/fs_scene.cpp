@@ -838,7 +838,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     mesh_out[mi].texcoords = nt > 0;
     mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
     if (!mesh_out[mi].tree) continue;
-    if (S.tris.size() + m.num_triangles > kMaxTriangles) {
+    if (S.tris.size() + S.deferred_tris + m.num_triangles > kMaxTriangles) {
       *err = "too many triangles for the 24-bit leaf encoding";
       return FS_ERR_INVALID;
     }
@@ -849,8 +849,8 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       DeferredMesh D;
       D.mesh = mi;
       D.num_tris = m.num_triangles;
-      D.node_base = (uint32_t)S.nodes.size();
-      D.tri_base = (uint32_t)S.tris.size();
+      S.deferred_nodes += m.num_triangles;  // bases are assigned after the host-built meshes
+      S.deferred_tris += m.num_triangles;
       D.lo.resize(3 * (size_t)m.num_triangles);
       D.hi.resize(3 * (size_t)m.num_triangles);
       parallel_chunks(m.num_triangles, [&](uint32_t, uint32_t f0, uint32_t f1) {
@@ -863,18 +863,9 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
           }
         }
       });
-      BvhNode zero;
-      std::memset(&zero, 0, sizeof(zero));
-      S.nodes.resize(S.nodes.size() + m.num_triangles, zero);
-      DevTri tz;
-      std::memset(&tz, 0, sizeof(tz));
-      S.tris.resize(S.tris.size() + m.num_triangles, tz);
-      if (any_normals) S.tri_normals.resize(S.tri_normals.size() + 12 * (size_t)m.num_triangles, 0.0f);
-      if (any_tex) S.tri_tex.resize(S.tri_tex.size() + 6 * (size_t)m.num_triangles, 0.0f);
       D.tris = std::move(mtris);
       if (any_normals) D.normals = std::move(mnormals);
       if (any_tex) D.tex = std::move(mtex);
-      mesh_out[mi].root = D.node_base;
       mesh_out[mi].root4 = -1;
       S.deferred.push_back(std::move(D));
       continue;
@@ -902,6 +893,20 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       return FS_ERR_INVALID;
     }
     mesh_out[mi].root4 = use4 ? Collapse4(S.nodes, &S.nodes4).run(mesh_out[mi].root) : -1;
+  }
+
+  // Device-built meshes take the node and triangle slots after the host arrays.
+  S.any_normals = any_normals;
+  S.any_tex = any_tex;
+  {
+    uint32_t nb = (uint32_t)S.nodes.size(), tb = (uint32_t)S.tris.size();
+    for (DeferredMesh& D : S.deferred) {
+      D.node_base = nb;
+      D.tri_base = tb;
+      mesh_out[D.mesh].root = nb;
+      nb += D.num_tris;
+      tb += D.num_tris;
+    }
   }
 
   // FS_PARK_MIN_TRIS lowers the parking threshold (tests exercise the SUSP

@@ -94,9 +94,11 @@ struct DevTri {
 static_assert(sizeof(DevTri) == 80, "DevTri layout");
 
 // A mesh whose BVH is built on the device (fs_upload_scene_ex with
-// FS_UPLOAD_GPU_BVH, fs_bvh_gpu.hip). prepare_scene reserves num_tris nodes
-// from node_base and num_tris triangle slots (plus normal/texcoord slots)
-// from tri_base in the scene arrays, and keeps the face-order inputs here.
+// FS_UPLOAD_GPU_BVH, fs_bvh_gpu.hip). Its node block (num_tris nodes from
+// node_base) and triangle slots (num_tris from tri_base, plus normal and
+// texcoord slots) follow the host-built arrays: the upload allocates them
+// on the device only (PreparedScene::deferred_nodes / deferred_tris), and
+// the face-order inputs wait here.
 struct DeferredMesh {
   uint32_t mesh = 0, num_tris = 0, node_base = 0, tri_base = 0;
   std::vector<float> lo, hi;  // 3 floats per face: the primitive box
@@ -119,6 +121,8 @@ struct PreparedScene {
   uint32_t max_depth = 0;
   double build_ms = 0.0;
   std::vector<DeferredMesh> deferred;  // meshes left for the device build
+  uint32_t deferred_nodes = 0, deferred_tris = 0;  // device-only slots after the host arrays
+  bool any_normals = false, any_tex = false;       // per-triangle normal / texcoord arrays exist
 };
 
 // Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
