@@ -24,6 +24,9 @@
 // Wave priority inside BVH walks (s_setprio): waves in a walk issue first,
 // so the dependent node fetches of the latency-bound walks start sooner
 // (C2 +1.3 %, C3 +0.8 %, C4 neutral; 1 and 3 measure the same; 0 = off)
+#ifndef FS_FLAT_LEAF  // leaf tests one triangle per trip over both leaves (A/B)
+#define FS_FLAT_LEAF 1
+#endif
 #ifndef FS_TRAV_PRIO
 #define FS_TRAV_PRIO 1
 #endif
@@ -1258,6 +1261,30 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       }
     }
     if (SUSP && susp) break;
+#if FS_FLAT_LEAF
+    // One triangle per lane per trip, running on through the leaves the walk
+    // stopped on (the popped far children may be leaves too), so a lane with
+    // 1+2 triangles costs the wave 3 trips, not max-per-leaf 2+2.
+    while (leaf) {
+#ifdef FS_PHASE_PROF
+      FS_WAVE_TRIP(tally.leaf_trips);
+      tally.lane_leaves++;
+#endif
+      uint32_t cnt = (leaf >> 24) & 0x7Fu;
+      if (cnt) {
+        test_leaf<COUNT, ZLMODE>(S, (leaf & 0x80FFFFFFu) | (1u << 24), oi, r, zl, h, tally);
+        cnt--;
+      }
+      if (cnt) {
+        leaf = kLeafBit | (cnt << 24) | ((leaf & 0xFFFFFFu) + 1u);
+      } else if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
+        leaf = w;
+        w = sp ? stk[--sp * kBlock] : kNone;
+      } else {
+        leaf = 0;
+      }
+    }
+#else
     while (leaf) {
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.leaf_trips);
@@ -1270,6 +1297,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         w = sp ? stk[--sp * kBlock] : kNone;
       }
     }
+#endif
     tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
   }
 #if FS_TRAV_PRIO

@@ -168,6 +168,49 @@ uint32_t leaf_target_env() {
   return (v && v <= kMaxLeafCount) ? v : 2u;
 }
 
+// FS_NODE_LAYOUT=pairs: sibling inner nodes share one 128-B line (an
+// even/odd slot pair), so the far child of a visited node arrives with the
+// near one. Node order never changes a hit (closest hit is a total order).
+bool pair_layout_env() {
+  const char* e = std::getenv("FS_NODE_LAYOUT");
+  return e && std::strcmp(e, "pairs") == 0;
+}
+
+// Rewrites the nodes [begin, end) of one mesh (root at begin, begin even) in
+// the pair layout: root, then per node (depth first) its inner children as
+// one aligned pair, padding with an unused slot where a pair would straddle.
+void relayout_pairs(std::vector<BvhNode>* nodes, uint32_t begin) {
+  std::vector<BvhNode> old(nodes->begin() + begin, nodes->end());
+  std::vector<BvhNode> out;
+  out.reserve(old.size() + old.size() / 8 + 2);
+  BvhNode blank;
+  std::memset(&blank, 0, sizeof(blank));
+  out.push_back(old[0]);
+  out.push_back(blank);
+  // (new index relative to begin, old index relative to begin)
+  std::vector<std::pair<uint32_t, uint32_t>> stack{{0u, 0u}};
+  while (!stack.empty()) {
+    auto [ni, oi] = stack.back();
+    stack.pop_back();
+    const BvhNode& o = old[oi];
+    uint32_t kids[2], nk = 0;
+    for (int c = 0; c < 2; c++)
+      if (!(o.child[c] & kLeafBit)) kids[nk++] = (uint32_t)c;
+    if (nk == 2 && (out.size() & 1u)) out.push_back(blank);
+    uint32_t slot[2];
+    for (uint32_t k = 0; k < nk; k++) {
+      slot[k] = (uint32_t)out.size();
+      out.push_back(old[o.child[kids[k]] - begin]);
+    }
+    BvhNode& n2 = out[ni];
+    for (uint32_t k = 0; k < nk; k++) n2.child[kids[k]] = begin + slot[k];
+    // Depth first, child 0's subtree first: push in reverse.
+    for (uint32_t k = nk; k-- > 0;) stack.push_back({slot[k], o.child[kids[k]] - begin});
+  }
+  nodes->resize(begin);
+  nodes->insert(nodes->end(), out.begin(), out.end());
+}
+
 // Subtrees are built concurrently down to this depth (2^depth threads);
 // FS_BVH_THREADS=1 builds sequentially (same tree, same layout).
 uint32_t parallel_depth_env() {
@@ -880,9 +923,17 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
       p.face = f;
     }
+    const bool pairs = !use4 && pair_layout_env();
+    if (pairs && (S.nodes.size() & 1u)) {
+      BvhNode blank;
+      std::memset(&blank, 0, sizeof(blank));
+      S.nodes.push_back(blank);
+    }
+    const uint32_t node_begin = (uint32_t)S.nodes.size();
     BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex);
     auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
+    if (pairs && mesh_out[mi].root == node_begin) relayout_pairs(&S.nodes, node_begin);
     if (std::getenv("FS_BUILD_LOG"))
       std::fprintf(stderr, "[fs build] mesh %u: %u tris, prepare %.1f ms, prims %.1f ms, bvh %.1f ms\n", mi,
                    m.num_triangles, std::chrono::duration<double, std::milli>(tp - t0).count(),

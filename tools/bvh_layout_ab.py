@@ -1,6 +1,9 @@
 """Render speed with the host-built vs the device-built BVH, interleaved.
 
-  python tools/bvh_layout_ab.py [scenes] [spp] [rounds]
+  python tools/bvh_layout_ab.py [scenes] [spp] [rounds] [variants]
+
+variants: comma list of host|device, each optionally with upload-time env
+settings, e.g. "host,host@FS_NODE_LAYOUT=pairs" (default "host,device").
 
 Two contexts on one GPU hold the same scene, one uploaded with the host SAH
 build and one with FS_UPLOAD_GPU_BVH; their renders alternate and every frame
@@ -21,6 +24,7 @@ def main():
     names = (sys.argv[1] if len(sys.argv) > 1 else "c4").split(",")
     spp = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    variants = (sys.argv[4] if len(sys.argv) > 4 else "host,device").split(",")
     W, H = 1920, 1080
     tmp = os.path.join(ROOT, "gpurun_out", "scenes")
     for name in names:
@@ -30,9 +34,20 @@ def main():
         fsamd.initialize_materials()
         cam = s.camera(0)
         ctx = {}
-        for b in ("host", "device"):
+        for b in variants:
+            builder, *extra = b.split("@")
+            saved = {}
+            for kv in extra:
+                k, v = kv.split("=", 1)
+                saved[k] = os.environ.get(k)
+                os.environ[k] = v
             r = fsamd.Renderer(0)
-            r.upload(s, gpu_bvh=b == "device")
+            r.upload(s, gpu_bvh=builder == "device")
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
             ctx[b] = (r, r.frame(W, H), r.scene_stats())
         res = {b: [] for b in ctx}
         ref = None

@@ -5,6 +5,6 @@ LIBS=$1; SC=${2:-c2,c3,c4}; SPP=${3:-32}; R=${4:-2}; MODE=${5:-auto}
 for i in $(seq 1 $R); do
   for L in $LIBS; do
     echo "== $L"
-    FSAMD_GPU_LIB=$PWD/$L timeout -k 10 200 python tools/perf_ab.py $MODE $SC $SPP 1 || exit 1
+    FSAMD_GPU_LIB=$PWD/$L timeout -k 10 ${AB_TIMEOUT:-150} python tools/perf_ab.py $MODE $SC $SPP 1 || exit 1
   done
 done
