@@ -89,7 +89,11 @@ def main():
     fsamd.initialize_materials()
     cam = scene.camera(0)
     gen_s = time.time() - t0
-    r = fsamd.Renderer(local_rank)
+    ndev = fsamd.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
+    device = local_rank if local_rank < ndev else local_rank % ndev  # a launcher may narrow visibility per rank
+    r = fsamd.Renderer(device)
     r.upload(scene, gpu_bvh=args.bvh == "device")
     stats = r.scene_stats()
     log(f"rank {rank}: scene {args.scene} written+loaded in {gen_s:.1f}s, BVH {stats}")
