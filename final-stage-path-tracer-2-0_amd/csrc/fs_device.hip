@@ -2669,6 +2669,14 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #ifndef FS_LEAN_WAVES
 #define FS_LEAN_WAVES 6
 #endif
+// The parked-walk (SUSP) kernel runs at 5 waves per SIMD: its parked state
+// and the second walk path need registers; 96 VGPRs cut its spills (C4 +2 %,
+// while the other kernels lose 4-7 % at 5).
+#ifndef FS_SUSP_WAVES
+#define FS_SUSP_WAVES 5
+#endif
+#define FS_STR2(x) #x
+#define FS_STR(x) FS_STR2(x)
 
 enum class KernelMode { kAuto, kLean, kLeanSusp, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
 
@@ -3087,8 +3095,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, false, false>";
       } else if (mode == KernelMode::kLeanSusp) {
         lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true, true>
-                   : dev::render_kernel_lean<false, FS_LEAN_WAVES, true, false, false, true, true>;
-        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, true>";
+                   : dev::render_kernel_lean<false, FS_SUSP_WAVES, true, false, false, true, true>;
+        ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_SUSP_WAVES) ", true, false, false, true, true>";
       } else if (mode == KernelMode::kLeanBvh4) {  // needs a scene uploaded with FS_BVH4=1
         lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
         ctx->last_kernel = "render_kernel_lean<false, 6, true, true, false, false, false>";

@@ -80,7 +80,8 @@ def test_scene_parity(name, dims, scene_dir, gpu_renderer):
     s = load_scene(name, scene_dir)
     out = gpu_render(gpu_renderer, s, s.camera(0), W, H, spp)
     # only C4 has a mesh large enough (>= 2^19 triangles) for parked walks
-    parked = gpu_renderer.last_kernel() == "render_kernel_lean<false, 6, true, false, false, true, true>"
+    k = gpu_renderer.last_kernel()
+    parked = k.startswith("render_kernel_lean<false, ") and k.endswith(", true, false, false, true, true>")
     assert parked == (name == "c4"), gpu_renderer.last_kernel()
     ref = oracle_render(s.desc_ptr(), s.camera(0), W, H, spp)
     assert_parity(out, ref, exact=True)
