@@ -2955,7 +2955,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_offset = params->tile_offset;
   L.tile_stride = stride;
   L.seed = params->seed;
-  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 8u;  // C4: 8 +2.2 % over 16
+  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 12u;  // C4 at 5 waves: 10-12 best
   // XCD placement (FS_XCD_BANDS): 0 dispatch order, 1 one band per XCD (C4 -25 %:
   // the bands are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
   L.xcd_bands = std::getenv("FS_XCD_BANDS") ? (uint32_t)std::atoi(std::getenv("FS_XCD_BANDS")) : 2u;
