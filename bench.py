@@ -37,10 +37,10 @@ WORKLOADS = {
     "c3": "~250k-triangle procedural atrium (BASELINE configs[2]) at 1920x1080, 1024 spp",
 }
 # Algorithmic bytes per unit of work, from the device SoA record
-# sizes: BVH node 64 B, triangle 80 B, analytic object record 128 B, per
+# sizes: BVH node 64 B, triangle 64 B (fs_scene.h DevTri), analytic object record 128 B, per
 # segment one material record (76 B) + one normal-table entry (16 B); per
 # sample 12 B of radiance.
-S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 80, 128, 92, 12
+S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
 
 
 def parse():

@@ -216,6 +216,55 @@ __device__ __forceinline__ void planar_bary(f4 pl, f3 v0, f3 v1, f3 vp, float& u
   v = (d00 * d12 - d01 * d02) * inv;
 }
 
+#if FS_TRI64
+// p1, v0, v1 hold the two components (a, b) the planar map keeps (fs_scene.h).
+struct TriData {
+  float p1a, p1b, v0a, v0b, v1a, v1b;
+  float d00, d01, d11, inv;
+  uint32_t axis, face;
+  f4 pl;
+};
+__device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
+  const float4* q = reinterpret_cast<const float4*>(T + i);
+  float4 a = q[0], b = q[1], c = q[2], d = q[3];
+  TriData t;
+  t.pl = mk4(a.x, a.y, a.z, a.w);
+  t.p1a = b.x;
+  t.p1b = b.y;
+  t.v0a = b.z;
+  t.v0b = b.w;
+  t.v1a = c.x;
+  t.v1b = c.y;
+  const uint32_t fa = __float_as_uint(c.z);
+  t.face = fa & 0x3FFFFFFFu;
+  t.axis = fa >> 30;
+  t.d00 = d.x;
+  t.d01 = d.y;
+  t.d11 = d.z;
+  t.inv = d.w;
+  return t;
+}
+__device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint32_t i) {
+  return T[i].face_axis & 0x3FFFFFFFu;
+}
+// intersect.cpp:146-177 with the triangle-only terms precomputed. The
+// reference's 3-term dot products over the planar-mapped vectors carry an
+// exact +0 term for the zeroed axis: ((0 + A) + B) for axis x, ((A + 0) + B)
+// for y and ((A + B) + 0) for z, restated here with the same rounding.
+__device__ __forceinline__ void bary_pre(const TriData& T, f3 pt, float& u, float& v) {
+  const bool az = T.axis == 2;
+  const float pa = T.axis == 0 ? pt.y : pt.x, pb = az ? pt.y : pt.z;
+  const float va = pa - T.p1a, vb = pb - T.p1b;
+  float A = T.v0a * va, B = T.v0b * vb;
+  const float d02 = (A + (az ? B : 0.0f)) + (az ? 0.0f : B);
+  A = T.v1a * va;
+  B = T.v1b * vb;
+  const float d12 = (A + (az ? B : 0.0f)) + (az ? 0.0f : B);
+  u = (T.d11 * d02 - T.d01 * d12) * T.inv;
+  v = (T.d00 * d12 - T.d01 * d02) * T.inv;
+}
+#define FS_BARY_ARG(pt, T) (pt)
+#else
 struct TriData {
   f3 p1, v0, v1;
   float d00, d01, d11, inv;
@@ -238,6 +287,7 @@ __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32
   t.pl = mk4(e.x, e.y, e.z, e.w);
   return t;
 }
+__device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint32_t i) { return T[i].face; }
 // intersect.cpp:146-177 with the triangle-only terms precomputed: vp is
 // planar-mapped like v0/v1 and the reference's dot products follow.
 __device__ __forceinline__ void bary_pre(const TriData& T, f3 vp, float& u, float& v) {
@@ -248,6 +298,8 @@ __device__ __forceinline__ void bary_pre(const TriData& T, f3 vp, float& u, floa
   u = (T.d11 * d02 - T.d01 * d12) * T.inv;
   v = (T.d00 * d12 - T.d01 * d02) * T.inv;
 }
+#define FS_BARY_ARG(pt, T) ((pt) - (T).p1)
+#endif
 
 // intersect.cpp:357-419 (non-zero-length branch)
 __device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t, f3& p, float& u, float& v) {
@@ -255,7 +307,7 @@ __device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t
   f3 pp;
   if (!ray_plane(T.pl, r, tt, pp)) return false;
   float uu, vv;
-  bary_pre(T, pp - T.p1, uu, vv);
+  bary_pre(T, FS_BARY_ARG(pp, T), uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     t = tt;
     p = pp;
@@ -271,7 +323,7 @@ __device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, 
   float d4 = T.pl.x * pt.x + T.pl.y * pt.y + T.pl.z * pt.z + T.pl.w * 1.0f;
   if (!cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) return false;
   float uu, vv;
-  bary_pre(T, pt - T.p1, uu, vv);
+  bary_pre(T, FS_BARY_ARG(pt, T), uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     u = uu;
     v = vv;
@@ -379,7 +431,7 @@ __device__ __forceinline__ void traverse_mesh(const DevScene& S, uint32_t root, 
           p = r.start;
         }
         if (hit) {
-          bool better = t < h.t || (t == h.t && h.obj == oi && face < S.tris[h.tri].face);
+          bool better = t < h.t || (t == h.t && h.obj == oi && face < tri_face(S.tris, h.tri));
           if (better) {
             h.t = t;
             h.p = p;
@@ -1103,7 +1155,7 @@ __device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, i
           t = 0.0f;
         }
         if (hit) {
-          bool better = t < h.t || (t == h.t && h.obj == oi && T.face < S.tris[h.prim].face);
+          bool better = t < h.t || (t == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
           if (better) {
             h.t = t;
             h.obj = oi;
@@ -1146,7 +1198,7 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
       t = 0.0f;
     }
     if (hit) {
-      bool better = t < h.t || (t == h.t && h.obj == oi && T.face < S.tris[h.prim].face);
+      bool better = t < h.t || (t == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
       if (better) {
         h.t = t;
         h.obj = oi;
@@ -1932,8 +1984,7 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
   p = h.point ? r.start : r.start + r.dir * h.t;
   int32_t kind = o->kind;
   if (kind == FS_OBJ_MESH) {
-    const float4* q = reinterpret_cast<const float4*>(S.tris + h.prim);
-    float4 pl = q[4];
+    const float4 pl = reinterpret_cast<const float4*>(S.tris + h.prim)[FS_TRI64 ? 0 : 4];  // face plane
     n = mk3(pl.x, pl.y, pl.z);
     if (o->i1) {
       const float4* nq = S.tri_normals + 3 * (size_t)h.prim;

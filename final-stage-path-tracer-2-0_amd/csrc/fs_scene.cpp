@@ -136,6 +136,25 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
   if (axis == 0) v0.x = v1.x = 0;
   if (axis == 1) v0.y = v1.y = 0;
   if (axis == 2) v0.z = v1.z = 0;
+  t->d00 = dot(v0, v0);
+  t->d01 = dot(v0, v1);
+  t->d11 = dot(v1, v1);
+  t->inv = 1 / (t->d00 * t->d11 - t->d01 * t->d01);
+  t->plane[0] = pl.x;
+  t->plane[1] = pl.y;
+  t->plane[2] = pl.z;
+  t->plane[3] = pl.w;
+#if FS_TRI64
+  const float P[3] = {p0.x, p0.y, p0.z}, A[3] = {v0.x, v0.y, v0.z}, B[3] = {v1.x, v1.y, v1.z};
+  const int ia = axis == 0 ? 1 : 0, ib = axis == 2 ? 1 : 2;
+  t->p1[0] = P[ia];
+  t->p1[1] = P[ib];
+  t->v0[0] = A[ia];
+  t->v0[1] = A[ib];
+  t->v1[0] = B[ia];
+  t->v1[1] = B[ib];
+  t->face_axis = (t->face_axis & 0x3FFFFFFFu) | (axis << 30);
+#else
   t->p1[0] = p0.x;
   t->p1[1] = p0.y;
   t->p1[2] = p0.z;
@@ -145,15 +164,8 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
   t->v1[0] = v1.x;
   t->v1[1] = v1.y;
   t->v1[2] = v1.z;
-  t->d00 = dot(v0, v0);
-  t->d01 = dot(v0, v1);
-  t->d11 = dot(v1, v1);
-  t->inv = 1 / (t->d00 * t->d11 - t->d01 * t->d01);
   t->axis = axis;
-  t->plane[0] = pl.x;
-  t->plane[1] = pl.y;
-  t->plane[2] = pl.z;
-  t->plane[3] = pl.w;
+#endif
 }
 
 constexpr int kMaxBins = 64;
@@ -853,7 +865,11 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       }
       DevTri& t = mtris[f];
       std::memset(&t, 0, sizeof(t));
+#if FS_TRI64
+      t.face_axis = f;
+#else
       t.face = f;
+#endif
       if (need) {
         f3 p0 = verts[vi[0]], p1 = verts[vi[1]], p2 = verts[vi[2]];
         fill_tri(&t, p0, p1, p2, plane_np(calc_normal(p0, p1, p2), p0));  // mesh.cpp:136-146

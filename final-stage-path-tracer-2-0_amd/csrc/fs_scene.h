@@ -72,12 +72,32 @@ constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
 // stack need exceeds the sum keeps the BVH2 (collapse4 checks).
 constexpr uint32_t kStackOverflow = 40;
 
-// Triangle record, 80 B: the operands of the reference test
-// (intersect.cpp:357-419) with every ray-independent term precomputed on the
-// host by the same float operations: p1, the planar-mapped edges v0 = p2-p1
-// and v1 = p3-p1 (dominant plane axis zeroed, intersect.cpp:96-129), their
-// dot products and 1/(d00*d11 - d01*d01) (:168-173), the face plane
-// (mesh.cpp:136-146, reversed winding) and the face index (tie-break).
+// Triangle record: the operands of the reference test (intersect.cpp:357-419)
+// with every ray-independent term precomputed on the host by the same float
+// operations: p1, the planar-mapped edges v0 = p2-p1 and v1 = p3-p1 (dominant
+// plane axis zeroed, intersect.cpp:96-129), their dot products and
+// 1/(d00*d11 - d01*d01) (:168-173), the face plane (mesh.cpp:136-146,
+// reversed winding) and the face index (tie-break).
+#ifndef FS_TRI64
+#define FS_TRI64 1
+#endif
+#if FS_TRI64
+// 64 B: the planar map zeroes one axis, so p1, v0 and v1 keep only the two
+// others, (a, b) = (axis == 0 ? y : x, axis == 2 ? y : z); face and axis
+// share a word (face | axis << 30).
+struct DevTri {
+  float plane[4];
+  float p1[2];
+  float v0[2];
+  float v1[2];
+  uint32_t face_axis;
+  uint32_t mesh_obj;
+  float d00, d01, d11, inv;
+};
+static_assert(sizeof(DevTri) == 64, "DevTri layout");
+inline uint32_t tri_face_host(const DevTri& t) { return t.face_axis & 0x3FFFFFFFu; }
+#else
+// 80 B: full 3-vectors (A/B builds with -DFS_TRI64=0).
 struct DevTri {
   float p1[3];
   uint32_t face;
@@ -92,6 +112,8 @@ struct DevTri {
   float plane[4];
 };
 static_assert(sizeof(DevTri) == 80, "DevTri layout");
+inline uint32_t tri_face_host(const DevTri& t) { return t.face; }
+#endif
 
 // A mesh whose BVH is built on the device (fs_upload_scene_ex with
 // FS_UPLOAD_GPU_BVH, fs_bvh_gpu.hip). Its node block (num_tris nodes from
