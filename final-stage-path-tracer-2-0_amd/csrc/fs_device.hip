@@ -2720,11 +2720,11 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #ifndef FS_LEAN_WAVES
 #define FS_LEAN_WAVES 6
 #endif
-// The parked-walk (SUSP) kernel runs at 5 waves per SIMD: its parked state
-// and the second walk path need registers; 96 VGPRs cut its spills (C4 +2 %,
-// while the other kernels lose 4-7 % at 5).
+// Waves per SIMD of the parked-walk (SUSP) kernel. 5 won (+2 % C4) while its
+// spills were 140 B/lane at 6; with the 64-B triangle record 6 wins again
+// (+2 % over 5).
 #ifndef FS_SUSP_WAVES
-#define FS_SUSP_WAVES 5
+#define FS_SUSP_WAVES 6
 #endif
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
@@ -3006,7 +3006,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_offset = params->tile_offset;
   L.tile_stride = stride;
   L.seed = params->seed;
-  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 12u;  // C4 at 5 waves: 10-12 best
+  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 10u;  // C4: 8-10 best at 6 waves, 10-12 at 5
   // XCD placement (FS_XCD_BANDS): 0 dispatch order, 1 one band per XCD (C4 -25 %:
   // the bands are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
   L.xcd_bands = std::getenv("FS_XCD_BANDS") ? (uint32_t)std::atoi(std::getenv("FS_XCD_BANDS")) : 2u;
