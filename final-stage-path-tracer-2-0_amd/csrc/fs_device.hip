@@ -14,6 +14,7 @@
 #include <memory>
 #include <string>
 #include <type_traits>
+#include <algorithm>
 #include <vector>
 
 #include "fs_bvh_gpu.h"
@@ -2076,6 +2077,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       t = vtile / P.groups;
       group = vtile - t * P.groups;
     }
+    if (P.tile_order) t = P.tile_order[t];
     rad_row = (group * P.owned + t) * micro_per_tile + micro;
     const uint32_t tile = P.tile_offset + t * P.tile_stride;
     const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -2522,11 +2524,13 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send,
+  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
       pack_recv, range_io;
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= kParkMinTris triangles: the SUSP schedule
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
+  std::vector<uint32_t> tile_order_host;  // the device tile_order buffer holds this order of ...
+  uint64_t tile_order_key[3] = {0, 0, 0};  // ... the tile set (offset, stride, owned; width, height) it was built for
   uint32_t last_launches = 0;    // trace-kernel launches of the last fs_render
   uint32_t last_launch_spp = 0;  // samples per pixel of its largest launch
   DevScene scene{};
@@ -2787,7 +2791,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
-                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv})
+                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order})
     b->release();
   ctx->wf.release();
   if (ctx->host_count) (void)hipHostFree(ctx->host_count);
@@ -3111,6 +3115,33 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.owned = owned;
   L.groups = 1;
   L.group_major = std::getenv("FS_GROUP_ORDER") ? (uint32_t)std::atoi(std::getenv("FS_GROUP_ORDER")) : 0u;
+  L.tile_order = nullptr;
+  if (pooled && owned > 1 && !(std::getenv("FS_TILE_ORDER") && std::atoi(std::getenv("FS_TILE_ORDER")) == 0)) {
+    // Longest jobs first: tiles nearer the image centre (where the scenes put
+    // their geometry) are dispatched first, so the launch tail runs on cheap
+    // edge tiles. Ties keep index order.
+    const uint64_t key[3] = {((uint64_t)L.tile_offset << 32) | L.tile_stride, owned,
+                             ((uint64_t)params->width << 32) | params->height};
+    std::vector<uint32_t>& ord = ctx->tile_order_host;
+    if (!std::equal(key, key + 3, ctx->tile_order_key)) {
+      ord.resize(owned);
+      std::vector<float> dist(owned);
+      const float cx = 0.5f * (float)params->width, cy = 0.5f * (float)params->height;
+      for (uint32_t i = 0; i < owned; i++) {
+        const uint32_t tile = L.tile_offset + i * L.tile_stride;
+        const float x = ((float)(tile % L.tiles_x) + 0.5f) * (float)ts - cx;
+        const float y = ((float)(tile / L.tiles_x) + 0.5f) * (float)ts - cy;
+        dist[i] = x * x + y * y;
+        ord[i] = i;
+      }
+      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return dist[a] < dist[b]; });
+      if ((rc = ensure(&ctx->tile_order, owned * sizeof(uint32_t)))) return rc;
+      FS_HIP(hipMemcpyAsync(ctx->tile_order.p, ord.data(), owned * sizeof(uint32_t), hipMemcpyHostToDevice,
+                            ctx->stream));
+      std::copy(key, key + 3, ctx->tile_order_key);
+    }
+    L.tile_order = (const uint32_t*)ctx->tile_order.p;
+  }
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
   if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)

@@ -81,6 +81,10 @@ struct Launch {
   uint32_t groups;
   uint32_t owned;  // 64x64 tiles this launch renders per group
   uint32_t group_major;  // block order: 0 a tile's groups together, 1 group by group (A/B)
+  // Dispatch order of the owned tiles (owned entries of owned-tile indices),
+  // or null for index order. Only the order changes: every tile keeps its
+  // radiance rows, so frames are identical.
+  const uint32_t* tile_order;
   uint64_t seed;
 };
 
