@@ -3021,7 +3021,11 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
   // Long renders are split into launches of at most `chunk` samples per
   // pixel; the running mean lives in the frame, so the result is identical.
-  const uint32_t chunk = kChunk;
+  // Samples per block: kChunk, or fewer by FS_CHUNK_RT (A/B). The kernel
+  // takes any per-block count up to kChunk (the radiance rows keep the
+  // kChunk stride).
+  uint32_t chunk = kChunk;
+  if (const char* e = std::getenv("FS_CHUNK_RT")) chunk = std::min<uint32_t>(kChunk, std::max(1, std::atoi(e)));
   // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
   // produces identical frames): "lean" path-regeneration megakernel with the
   // unwind scratch in HBM rows, while-while traversal and the wave's
