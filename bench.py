@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-tile-stride", type=int, default=4, help="CPU sample renders 1/stride of the tiles")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads; 0 = one per hardware thread this process may run on "
+                         "(the reference's hardware_concurrency() bands, engine.cpp:174,261-274)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scene-dir", default=None)
     ap.add_argument("--bvh", default="device", choices=["device", "host"],
@@ -197,6 +199,24 @@ def main():
         dist.destroy_process_group()
 
 
+def host_cpus():
+    """nproc, the CPUs this process may run on, and the cgroup CPU quota
+    (cpu.max, in CPUs; None if unlimited) of the host that times the baseline."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": nproc, "affinity": aff, "quota": quota}
+
+
 def cpu_baseline(args, scene, cam):
     """The oracle (CPU port of the reference algorithm, reference octree)
     timed on a bounded tile subset of the same workload."""
@@ -209,7 +229,8 @@ def cpu_baseline(args, scene, cam):
         build = time.time() - t
         stride = args.cpu_tile_stride
         p = fsamd.render_params(args.width, args.height, args.cpu_spp, tile_stride=stride, tile_offset=0)
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        hw = host_cpus()
+        threads = args.cpu_threads if args.cpu_threads > 0 else hw["affinity"]
         t = time.perf_counter()
         f = o.render(cam, p, threads=threads)
         dt = time.perf_counter() - t
@@ -224,9 +245,12 @@ def cpu_baseline(args, scene, cam):
         except OSError:
             pass
         return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+                "nproc": hw["nproc"], "affinity_cpus": hw["affinity"], "cgroup_cpu_quota": hw["quota"],
                 "sample": f"{args.scene} {args.width}x{args.height}, 1/{stride} of the 64x64 tiles, "
                           f"{args.cpu_spp} spp = {n} samples in {dt:.1f}s (octree build {build:.1f}s excluded)",
-                "cpu": cpu_model or platform.processor()}
+                "cpu": cpu_model or platform.processor(),
+                "calibration": "restatement/reference rate 1.03 on C4 1080p (8 threads, survey container; "
+                               "DESIGN §6): the baseline stands for the reference on C4 only"}
     except Exception as e:  # the baseline is reported, never required
         log(f"cpu baseline failed: {e}")
         return None

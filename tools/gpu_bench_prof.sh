@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profiling script (runs on the GPU box from the repo root).
 set -o pipefail
-R=${1:-r01}
+R=${1:-r02}
 mkdir -p gpurun_out/$R
 export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$R/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/$R/smoke.log; exit 1; }
