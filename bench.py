@@ -9,6 +9,11 @@ frame; for N > 1 the frame's 64x64 tiles are dealt round-robin to the ranks
 and gathered to rank 0 with RCCL (ncclGather over xGMI) inside the step.
 Rank 0 prints one JSON line. Scene load/BVH build are outside the timed
 region (reported in config).
+
+The GPU processes never import torch: its wheel bundles a second HIP runtime
+(libamdhip64) that must not share a process with libfsgpu.so's. The control
+plane for N > 1 (RCCL unique id, barriers, the max over ranks) goes through
+rendezvous.FileGroup, files in a directory the launcher's ranks share.
 """
 from __future__ import annotations
 
@@ -24,9 +29,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "final-stage-path-tracer-2-0_amd")
 sys.path.insert(0, PKG)
 
-# Load the HIP layer before anything else can pull in another HIP runtime.
 import fsamd  # noqa: E402
+import rendezvous  # noqa: E402
 import scenes  # noqa: E402
+
+# The HIP layer (libfsgpu.so + libfshost.so) is loaded here, first.
+fsamd.gpu_lib()
+fsamd.host_lib()
 
 METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080, 1024spp; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -75,13 +84,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dist = None
-    if world > 1:
-        import torch  # noqa: F401  (CPU-only use: gloo control plane)
-        import torch.distributed as dist_mod
-
-        dist = dist_mod
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    group = rendezvous.FileGroup(rank, world) if world > 1 else None
 
     scene_dir = args.scene_dir or os.path.join(tempfile.gettempdir(), f"fs_bench_{os.getuid()}_r{rank}")
     t0 = time.time()
@@ -102,13 +105,9 @@ def main():
     W, H, spp = args.width, args.height, args.spp
     frame = r.frame(W, H)
     params = fsamd.render_params(W, H, spp, tile_offset=rank, tile_stride=world)
-    if world > 1:
-        import torch
-
-        uid = bytearray(fsamd.Renderer.comm_unique_id() if rank == 0 else bytes(128))
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        r.comm_init(world, rank, bytes(t.tolist()))
+    if group:
+        uid = group.broadcast(fsamd.Renderer.comm_unique_id() if rank == 0 else None, root=0)
+        r.comm_init(world, rank, uid)
 
     def step():
         frame.reset()
@@ -123,8 +122,8 @@ def main():
         log(f"rank {rank}: warmup {i} render {ms:.1f} ms")
 
     def barrier():
-        if dist:
-            dist.barrier()
+        if group:
+            group.barrier()
 
     barrier()
     r.synchronize()
@@ -138,12 +137,8 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_name = r.last_kernel()
     launches, launch_spp = r.last_launches()
-    if dist:
-        import torch
-
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    if group:
+        elapsed = group.max(elapsed)
 
     # ---- roofline of the trace kernel: algorithmic bytes from a counted launch
     total_samples = W * H * spp * args.steps
@@ -195,8 +190,8 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    if group:
+        group.close()
 
 
 def host_cpus():

@@ -26,6 +26,7 @@ struct GpuBvhJob {
   const float* normals;  // 12 floats per triangle, or null
   const float* tex;      // 6 floats per triangle, or null
   uint32_t num_tris, leaf, node_base, tri_base;
+  bool log;  // fs_options.build_log: per-phase wall time to stderr
 };
 
 struct GpuBvhResult {

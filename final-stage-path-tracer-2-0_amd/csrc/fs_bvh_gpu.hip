@@ -757,7 +757,7 @@ int gpu_build_mesh_bvh(hipStream_t stream, const GpuBvhJob& job, BvhNode* d_node
     }
   B.lo = lo;
   B.hi = hi;
-  const bool log = std::getenv("FS_BUILD_LOG") != nullptr;
+  const bool log = job.log;
   auto t0 = std::chrono::steady_clock::now();
   auto stamp = [&](const char* what) -> int {  // FS_BUILD_LOG: per-phase wall time
     if (!log) return FS_OK;

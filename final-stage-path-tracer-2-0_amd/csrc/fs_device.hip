@@ -43,14 +43,6 @@ struct Ray {
   f3 start, stop, dir;
 };
 
-struct Hit {
-  float t;
-  f3 p, n;
-  int32_t mat;
-  int32_t obj;
-  uint32_t tri;  // global triangle index of a mesh hit
-  float u, v;
-};
 
 __device__ __forceinline__ bool zero_len(const Ray& r) {  // trace.cpp:16
   return cmp_eps(length(r.dir), 0.0f, kEpsilon);
@@ -352,199 +344,6 @@ struct Tally {
   } while (0)
 #endif
 
-// Traverses one mesh's BVH2 (conservative culling) and applies the
-// reference leaf rule: a face replaces the current hit iff t < best, or on an
-// exact tie within the same mesh iff its face index is lower (the order in
-// which mesh.cpp:89-110 would meet the two faces in one octree leaf).
-template <bool COUNT>
-__device__ __forceinline__ void traverse_mesh(const DevScene& S, uint32_t root, int32_t oi, int32_t mat,
-                                              const Ray& r, bool zl, Hit& h, uint32_t* __restrict__ stk,
-                                              Tally<COUNT>& tally) {
-  const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
-  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
-  uint32_t w = root;
-  uint32_t sp = 0;
-  for (;;) {
-    if (!(w & kLeafBit)) {
-      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
-      float4 X = q[0], Y = q[1], Z = q[2];
-      uint4 C = reinterpret_cast<const uint4*>(q)[3];
-      if (COUNT) tally.nodes++;
-      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
-      bool h0, h1;
-      float t0, t1;
-      if (!zl) {
-        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
-        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
-        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
-        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
-        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
-        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
-        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
-        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
-        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
-        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
-        h0 = n0 <= f0;
-        h1 = n1 <= f1;
-        t0 = n0;
-        t1 = n1;
-      } else {  // a point: visit every box that contains it
-        f3 s = r.start;
-        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
-        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
-        t0 = t1 = 0.0f;
-      }
-      if (h0 && h1) {
-        uint32_t nearw = t1 < t0 ? C.y : C.x;
-        uint32_t farw = t1 < t0 ? C.x : C.y;
-        stk[sp * kBlock] = farw;
-        sp++;
-        w = nearw;
-        continue;
-      }
-      if (h0) {
-        w = C.x;
-        continue;
-      }
-      if (h1) {
-        w = C.y;
-        continue;
-      }
-    } else {
-      uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
-      for (uint32_t i = 0; i < cnt; i++) {
-        uint32_t ti = first + i;
-        TriData T = load_tri(S.tris, ti);
-        uint32_t face = T.face;
-        if (COUNT) tally.tris++;
-        float t, u, v;
-        f3 p;
-        bool hit;
-        if (!zl) {
-          hit = ray_tri(T, r, t, p, u, v);
-        } else {
-          hit = point_in_tri(T, r.start, u, v);
-          t = 0.0f;
-          p = r.start;
-        }
-        if (hit) {
-          bool better = t < h.t || (t == h.t && h.obj == oi && face < tri_face(S.tris, h.tri));
-          if (better) {
-            h.t = t;
-            h.p = p;
-            h.n = xyz(T.pl);
-            h.mat = mat;
-            h.obj = oi;
-            h.tri = ti;
-            h.u = u;
-            h.v = v;
-          }
-        }
-      }
-    }
-    if (sp == 0) break;
-    sp--;
-    w = stk[sp * kBlock];
-  }
-}
-
-// Scene::Trace (scene.cpp:227-249) over the object list.
-template <bool COUNT>
-__device__ bool scene_trace(const DevScene& S, const Ray& r, Hit& h, uint32_t* __restrict__ stk,
-                            Tally<COUNT>& tally) {
-  h.t = 2.0f;
-  h.p = mk3(0, 0, 0);
-  h.n = mk3(0, 0, 0);
-  h.mat = -1;
-  h.obj = -1;
-  h.tri = 0;
-  h.u = h.v = 0.0f;
-  bool zl = zero_len(r);
-  bool detected = false;
-  for (uint32_t oi = 0; oi < S.num_objects; ++oi) {
-    const DevObject* __restrict__ o = S.objects + oi;
-    int32_t kind = o->kind, mat = o->mat;
-    const float* d = o->d;
-    if (kind == FS_OBJ_MESH) {
-      if (!o->i2) continue;
-      // MeshBvhNode::Trace root test (mesh.cpp:79-83), restated exactly: the
-      // reference skips the mesh when the root box "param" exceeds the best.
-      if (!ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) continue;
-      float before = h.t;
-      int32_t before_obj = h.obj;
-      traverse_mesh<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, mat, r, zl, h, stk, tally);
-      if (h.t != before || h.obj != before_obj) detected = true;
-      continue;
-    }
-    if (zl) continue;  // analytic objects never report a hit for a zero-length ray
-    if (COUNT) tally.prims++;
-    float t;
-    f3 p, n;
-    if (kind == FS_OBJ_SPHERE) {  // object.cpp:23-36
-      if (ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n) && t < h.t) {
-        h.t = t; h.p = p; h.n = n; h.mat = mat; h.obj = (int32_t)oi;
-        detected = true;
-      }
-    } else if (kind == FS_OBJ_PLANE) {  // object.cpp:59-73
-      f4 pl = mk4(d[0], d[1], d[2], d[3]);
-      if (ray_plane(pl, r, t, p) && t < h.t) {
-        h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
-        detected = true;
-      }
-    } else if (kind == FS_OBJ_DISC) {  // object.cpp:97-113
-      f4 pl = mk4(d[0], d[1], d[2], d[3]);
-      if (ray_plane(pl, r, t, p)) {
-        if (length(mk3(d[4], d[5], d[6]) - p) <= d[7] && t < h.t) {
-          h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
-          detected = true;
-        }
-      }
-    } else if (kind == FS_OBJ_QUAD_ONWH) {  // object.cpp:213-237
-      f4 pl = mk4(d[0], d[1], d[2], d[3]);
-      if (ray_plane(pl, r, t, p)) {
-        f3 ph = p - mk3(d[4], d[5], d[6]);
-        float td = dot(mk3(d[12], d[13], d[14]), ph);
-        float bd = dot(mk3(d[9], d[10], d[11]), ph);
-        if (!(fabsf(bd) > d[7] || fabsf(td) > d[8]) && t < h.t) {
-          h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
-          detected = true;
-        }
-      }
-    } else if (kind == FS_OBJ_CUBOID) {  // object.cpp:126-165
-      for (uint32_t i = 0; i < 6; i++) {
-        f4 pl = mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
-        if (ray_plane(pl, r, t, p) && t < h.t) {
-          bool ok = true;
-          for (uint32_t j = 0; j < 6; j++) {
-            if (i / 2 != j / 2 && plane_dist(mk4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]), p) > 0.0f) {
-              ok = false;
-              break;
-            }
-          }
-          if (ok) {
-            h.t = t; h.p = p; h.n = xyz(pl); h.mat = mat; h.obj = (int32_t)oi;
-            detected = true;
-          }
-        }
-      }
-    }
-  }
-  if (detected && h.obj >= 0 && S.objects[h.obj].kind == FS_OBJ_MESH && S.objects[h.obj].i1) {
-    // MeshObject::Trace interpolated (unnormalised) normal, mesh.cpp:289-298
-    const float4* nq = S.tri_normals + 3 * (size_t)h.tri;
-    float4 a = nq[0], b = nq[1], c = nq[2];
-    f3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(b.x, b.y, b.z), n2 = mk3(c.x, c.y, c.z);
-    h.n = n0 + (n1 - n0) * h.u + (n2 - n0) * h.v;
-  }
-  f4 cp = plane_np(h.n, h.p);
-  if (plane_dist(cp, r.start) < 0.0f) h.n = h.n * (float)-1.0;
-  return detected;
-}
-
 // normal_sphere (normal.cpp:29-105)
 __device__ __forceinline__ f3 table_normal(const DevScene& S, uint64_t& rng) {
   float4 q = S.table[rng_table_index(rng)];
@@ -727,341 +526,9 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t 
   return L;
 }
 
-template <bool COUNT>
-__device__ f3 trace_sample(const DevScene& S, const DevCamera& C, float fx, float fy, uint64_t rng, Aov& aov,
-                           uint32_t* __restrict__ stk, float2* __restrict__ lvl, Tally<COUNT>& tally,
-                           uint32_t& segments) {
-  Ray r = camera_ray(C, fx, fy, rng);
-
-  // ---- forward pass: TraceStep recursion descending (engine.cpp:59-138)
-  uint32_t mats_lo = 0, mats_hi = 0;
-  f3 L = mk3(0, 0, 0);
-  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-  int top = -1;
-  for (uint32_t depth = 0;; depth++) {
-    if (depth >= kMaxDepth) {
-      L = mk3(0, 0, 0);
-      break;
-    }
-    if (C.fast_render && depth > 1) {
-      L = mk3(1, 1, 1);
-      break;
-    }
-    segments++;
-    Hit h;
-    if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
-      if (depth == 1) lp0 = r.stop;
-      L = mk3(S.sky_r, S.sky_g, S.sky_b);
-      if (depth == 0) {
-        aov.normal = normalize(r.dir);
-        aov.id = S.sky_id;
-        aov.depth = C.z_far;
-      }
-      break;
-    }
-    if (depth == 1) lp0 = h.p;
-    const fs_material& m = S.materials[h.mat];
-    int32_t kind = m.kind;
-    f3 view = normalize(h.p - r.start);
-    f3 refl = mat_reflection(S, m, view, h.n, rng);
-    float c = fmaxf(0.0f, dot(h.n, refl));
-    float ds = 0.0f;
-    if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
-      f3 hv = normalize(view * (float)-1.0 + refl);
-      ds = pow50(dot(hv, h.n));
-    }
-    lvl[depth * kBlock] = make_float2(c, ds);
-    if (depth < 4)
-      mats_lo |= (uint32_t)h.mat << (8 * depth);
-    else
-      mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
-    top = (int)depth;
-    if (depth == 0) {
-      p0 = h.p;
-      aov.normal = h.n;
-      aov.id = m.id;
-      aov.depth = length(r.start - h.p);
-    }
-    Ray nr;  // engine.cpp:120-127
-    nr.start = h.p;
-    nr.stop = h.p + refl * C.z_far;
-    nr.dir = nr.stop - nr.start;
-    f3 off = refl * kStepOffset;
-    nr.start = nr.start + off;
-    nr.dir = nr.dir - off;
-    if (!mat_will_use(m, refl, h.n)) {
-      L = mk3(0, 0, 0);
-      break;
-    }
-    r = nr;
-  }
-
-  return unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng);
-}
-
 __device__ __forceinline__ uint8_t gamma8(float c) {  // frame.cpp:67-71
   float s = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
   return (uint8_t)(255.0 * pow((double)s, 1.0 / 2.2) + 0.5);
-}
-
-// One block = one wave64 = one 8x8 pixel block of an owned tile; each lane
-// walks its pixel's samples in order, applying DisplayFrame::WritePixel's
-// running mean after each (frame.cpp:53-63).
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevFrame F, Launch P,
-                                                         DevCounters* __restrict__ counters) {
-  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
-  __shared__ float2 lvl_all[kMaxDepth * kBlock];
-  const uint32_t lane = threadIdx.x;
-  uint32_t* stk = stk_all + lane;
-  float2* lvl = lvl_all + lane;
-
-  const uint32_t micro_per_side = P.tile_size / 8;
-  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
-  const uint32_t owned = blockIdx.x / micro_per_tile;
-  const uint32_t micro = blockIdx.x % micro_per_tile;
-  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
-  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const uint32_t x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
-  const uint32_t y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
-  if (x >= F.width || y >= F.height) return;
-
-  const size_t pix = (size_t)y * F.width + x;
-  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
-  uint32_t n = F.count[pix];
-  Aov aov;
-  aov.normal = mk3(0, 0, 0);
-  aov.depth = 0.0f;
-  aov.id = 0;
-  Tally<COUNT> tally;
-  uint32_t segments = 0;
-  for (uint32_t s = 0; s < P.spp; s++) {
-    uint64_t rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
-    f3 L = trace_sample<COUNT>(S, C, (float)x, (float)y, rng, aov, stk, lvl, tally, segments);
-    f3 np = mean * (float)n + L;
-    float dv = (float)(++n);
-    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-  }
-  F.color[3 * pix] = mean.x;
-  F.color[3 * pix + 1] = mean.y;
-  F.color[3 * pix + 2] = mean.z;
-  F.count[pix] = n;
-  F.display[3 * pix] = gamma8(mean.x);
-  F.display[3 * pix + 1] = gamma8(mean.y);
-  F.display[3 * pix + 2] = gamma8(mean.z);
-  if (P.spp) {
-    F.normal[3 * pix] = aov.normal.x;
-    F.normal[3 * pix + 1] = aov.normal.y;
-    F.normal[3 * pix + 2] = aov.normal.z;
-    F.depth[pix] = aov.depth;
-    F.material[pix] = aov.id;
-  }
-  if (COUNT) {
-    atomicAdd(&counters->samples, (unsigned long long)P.spp);
-    atomicAdd(&counters->segments, (unsigned long long)segments);
-    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
-  }
-}
-
-
-// Path regeneration: one loop iteration traces ONE ray segment for every
-// active lane; a lane whose path ended unwinds it, folds it into the running
-// mean and starts its pixel's next sample at once, so a wave never idles
-// waiting for its longest path (the forward/backward split keeps the
-// reference's rounding). Same outputs as render_kernel, bit for bit.
-template <bool COUNT, int WAVES>
-__global__ __launch_bounds__(kBlock, WAVES) void render_kernel_regen(DevScene S, DevCamera C, DevFrame F, Launch P,
-                                                               DevCounters* __restrict__ counters) {
-  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
-  __shared__ float2 lvl_all[kMaxDepth * kBlock];
-  const uint32_t lane = threadIdx.x;
-  uint32_t* stk = stk_all + lane;
-  float2* lvl = lvl_all + lane;
-
-  const uint32_t micro_per_side = P.tile_size / 8;
-  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
-  const uint32_t owned = blockIdx.x / micro_per_tile;
-  const uint32_t micro = blockIdx.x % micro_per_tile;
-  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
-  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const uint32_t x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
-  const uint32_t y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
-  if (x >= F.width || y >= F.height) return;
-
-  const size_t pix = (size_t)y * F.width + x;
-  const float fx = (float)x, fy = (float)y;
-  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
-  uint32_t n = F.count[pix];
-  Aov aov;
-  aov.normal = mk3(0, 0, 0);
-  aov.depth = 0.0f;
-  aov.id = 0;
-  Tally<COUNT> tally;
-  uint32_t segments = 0;
-
-  uint32_t s = 0;
-  uint64_t rng = 0;
-  Ray r;
-  uint32_t depth = 0, mats_lo = 0, mats_hi = 0;
-  int top = -1;
-  f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-  bool fresh = true;
-  while (s < P.spp) {
-    if (fresh) {  // TracePixel for sample s (engine.cpp:161-164)
-      rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
-      r = camera_ray(C, fx, fy, rng);
-      depth = 0;
-      mats_lo = mats_hi = 0;
-      top = -1;
-      p0 = lp0 = mk3(0, 0, 0);
-      fresh = false;
-    }
-    // ---- one TraceStep level (engine.cpp:62-138)
-    bool done = false;
-    f3 L;
-    if (depth >= kMaxDepth) {
-      L = mk3(0, 0, 0);
-      done = true;
-    } else if (C.fast_render && depth > 1) {
-      L = mk3(1, 1, 1);
-      done = true;
-    } else {
-      segments++;
-      Hit h;
-      if (!scene_trace<COUNT>(S, r, h, stk, tally)) {
-        if (depth == 1) lp0 = r.stop;
-        L = mk3(S.sky_r, S.sky_g, S.sky_b);
-        if (depth == 0) {
-          aov.normal = normalize(r.dir);
-          aov.id = S.sky_id;
-          aov.depth = C.z_far;
-        }
-        done = true;
-      } else {
-        if (depth == 1) lp0 = h.p;
-        const fs_material& m = S.materials[h.mat];
-        int32_t kind = m.kind;
-        f3 view = normalize(h.p - r.start);
-        f3 refl = mat_reflection(S, m, view, h.n, rng);
-        float c = fmaxf(0.0f, dot(h.n, refl));
-        float ds = 0.0f;
-        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {  // material.cpp:277-281
-          f3 hv = normalize(view * (float)-1.0 + refl);
-          ds = pow50(dot(hv, h.n));
-        }
-        lvl[depth * kBlock] = make_float2(c, ds);
-        if (depth < 4)
-          mats_lo |= (uint32_t)h.mat << (8 * depth);
-        else
-          mats_hi |= (uint32_t)h.mat << (8 * (depth - 4));
-        top = (int)depth;
-        if (depth == 0) {
-          p0 = h.p;
-          aov.normal = h.n;
-          aov.id = m.id;
-          aov.depth = length(r.start - h.p);
-        }
-        bool use = mat_will_use(m, refl, h.n);
-        Ray nr;  // engine.cpp:120-127
-        nr.start = h.p;
-        nr.stop = h.p + refl * C.z_far;
-        nr.dir = nr.stop - nr.start;
-        f3 off = refl * kStepOffset;
-        nr.start = nr.start + off;
-        nr.dir = nr.dir - off;
-        r = nr;
-        if (!use) {
-          L = mk3(0, 0, 0);
-          done = true;
-        } else {
-          depth++;
-        }
-      }
-    }
-    if (done) {  // ---- return path of the recursion + DisplayFrame::WritePixel
-      L = unwind(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng);
-      f3 np = mean * (float)n + L;
-      float dv = (float)(++n);
-      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-      s++;
-      fresh = true;
-    }
-  }
-  F.color[3 * pix] = mean.x;
-  F.color[3 * pix + 1] = mean.y;
-  F.color[3 * pix + 2] = mean.z;
-  F.count[pix] = n;
-  F.display[3 * pix] = gamma8(mean.x);
-  F.display[3 * pix + 1] = gamma8(mean.y);
-  F.display[3 * pix + 2] = gamma8(mean.z);
-  if (P.spp) {
-    F.normal[3 * pix] = aov.normal.x;
-    F.normal[3 * pix + 1] = aov.normal.y;
-    F.normal[3 * pix + 2] = aov.normal.z;
-    F.depth[pix] = aov.depth;
-    F.material[pix] = aov.id;
-  }
-  if (COUNT) {
-    atomicAdd(&counters->samples, (unsigned long long)P.spp);
-    atomicAdd(&counters->segments, (unsigned long long)segments);
-    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
-  }
-}
-
-
-// ============================================================================
-// Wavefront path tracer: extend (traversal only, high occupancy) and shade
-// (materials, RNG, next ray, accumulation) kernels over a compacted list of
-// live paths. One path slot per owned pixel; a slot walks its pixel's
-// samples in order, so the running mean is the reference's.
-// ============================================================================
-struct WfHit {
-  float t, u, v;
-  int32_t obj;    // -1: miss
-  uint32_t prim;  // mesh: global triangle; cuboid: face
-  uint32_t point; // 1: zero-length ray hit (point = ray start)
-  uint32_t pad0, pad1;
-};
-
-struct WfState {
-  uint32_t* pixel;
-  float4* ray0;  // start.xyz, dir.x
-  float4* ray1;  // dir.y, dir.z, stop.x, stop.y
-  float* ray2;   // stop.z
-  WfHit* hit;
-  uint64_t* rng;
-  uint4* path;   // depth, top, mats_lo, mats_hi
-  float4* p0;    // p0.xyz, lp0.x
-  float2* lp0;   // lp0.y, lp0.z
-  float2* lvl;   // kMaxDepth per slot
-  float4* acc;   // mean.xyz, count (bits)
-  uint32_t* samples;
-  float4* aov;   // normal.xyz, depth
-  uint64_t* aov_id;
-  uint32_t* list0;
-  uint32_t* list1;
-  uint32_t* ovf;    // lean megakernel: BVH4 stack overflow rows
-  float4* tex;      // lean megakernel: per-level texel rows (textured scenes)
-  float* rad;       // lean megakernel (pooled): per-sample radiance rows
-  uint32_t* count;  // [0], [1]: active counts
-};
-
-__device__ __forceinline__ Ray wf_load_ray(const WfState& W, uint32_t slot) {
-  float4 a = W.ray0[slot], b = W.ray1[slot];
-  Ray r;
-  r.start = mk3(a.x, a.y, a.z);
-  r.dir = mk3(a.w, b.x, b.y);
-  r.stop = mk3(b.z, b.w, W.ray2[slot]);
-  return r;
-}
-__device__ __forceinline__ void wf_store_ray(const WfState& W, uint32_t slot, const Ray& r) {
-  W.ray0[slot] = make_float4(r.start.x, r.start.y, r.start.z, r.dir.x);
-  W.ray1[slot] = make_float4(r.dir.y, r.dir.z, r.stop.x, r.stop.y);
-  W.ray2[slot] = r.stop.z;
 }
 
 // Object records are wave-uniform and never written by a kernel: reading
@@ -1086,93 +553,6 @@ struct WalkSuspend {
   int32_t oi = -1;  // -1: no suspended walk
   uint32_t w = 0, leaf = 0, sp = 0;
 };
-
-// BVH2 traversal of one mesh, closest-hit bookkeeping only (no point/normal).
-template <bool COUNT>
-__device__ __forceinline__ void traverse_min(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
-                                             MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally) {
-  const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
-  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
-  uint32_t w = root;
-  uint32_t sp = 0;
-  for (;;) {
-    if (!(w & kLeafBit)) {
-      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
-      float4 X = q[0], Y = q[1], Z = q[2];
-      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
-      if (COUNT) tally.nodes++;
-      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
-      bool h0, h1;
-      float t0, t1;
-      if (!zl) {
-        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
-        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
-        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
-        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
-        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
-        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
-        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
-        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
-        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
-        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
-        h0 = n0 <= f0;
-        h1 = n1 <= f1;
-        t0 = n0;
-        t1 = n1;
-      } else {
-        f3 s = r.start;
-        h0 = s.x >= X.x && s.x <= X.z && s.y >= Y.x && s.y <= Y.z && s.z >= Z.x && s.z <= Z.z;
-        h1 = s.x >= X.y && s.x <= X.w && s.y >= Y.y && s.y <= Y.w && s.z >= Z.y && s.z <= Z.w;
-        t0 = t1 = 0.0f;
-      }
-      if (h0 && h1) {
-        bool swap = t1 < t0;
-        stk[sp * kBlock] = swap ? Cw.x : Cw.y;
-        sp++;
-        w = swap ? Cw.y : Cw.x;
-        continue;
-      }
-      if (h0 || h1) {
-        w = h0 ? Cw.x : Cw.y;
-        continue;
-      }
-    } else {
-      uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
-      for (uint32_t i = 0; i < cnt; i++) {
-        uint32_t ti = first + i;
-        TriData T = load_tri(S.tris, ti);
-        if (COUNT) tally.tris++;
-        float t, u, v;
-        bool hit;
-        if (!zl) {
-          f3 p;
-          hit = ray_tri(T, r, t, p, u, v);
-        } else {
-          hit = point_in_tri(T, r.start, u, v);
-          t = 0.0f;
-        }
-        if (hit) {
-          bool better = t < h.t || (t == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
-          if (better) {
-            h.t = t;
-            h.obj = oi;
-            h.prim = ti;
-            h.u = u;
-            h.v = v;
-            h.point = zl ? 1u : 0u;
-          }
-        }
-      }
-    }
-    if (sp == 0) break;
-    sp--;
-    w = stk[sp * kBlock];
-  }
-}
 
 // The same traversal restructured as while-while with postponed leaves
 // (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking
@@ -1365,107 +745,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   return SUSP && susp;
 }
 
-// Scene::Trace closest hit (scene.cpp:227-237) without the hit geometry.
-// Per-lane traversal stack: kTraversalStack entries in LDS (column per lane),
-// deeper entries in a per-lane HBM row (BVH4 only; rarely touched).
-struct LaneStack {
-  uint32_t* lds;  // stk_all + lane, stride kBlock
-  uint32_t* ovf;  // wave row base + lane, stride kBlock
-  __device__ __forceinline__ void push(uint32_t& sp, uint32_t v) const {
-    if (sp < kTraversalStack)
-      lds[sp * kBlock] = v;
-    else
-      ovf[(sp - kTraversalStack) * kBlock] = v;
-    sp++;
-  }
-  __device__ __forceinline__ uint32_t pop(uint32_t& sp, uint32_t none) const {
-    if (sp == 0) return none;
-    --sp;
-    return sp < kTraversalStack ? lds[sp * kBlock] : ovf[(sp - kTraversalStack) * kBlock];
-  }
-};
-
-// BVH4 closest-hit traversal, while-while with postponed leaves as
-// traverse_ww. The hit children are ordered near to far by a 4-input sorting
-// network; the nearest is taken next and the rest pushed far-first.
-template <bool COUNT>
-__device__ __forceinline__ void traverse4_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl,
-                                             MinHit& h, const LaneStack& st, Tally<COUNT>& tally) {
-  constexpr uint32_t kNone = 0x7FFFFFFFu;
-  const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
-  float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-  float ox = -r.start.x * ix, oy = -r.start.y * iy, oz = -r.start.z * iz;
-  uint32_t w = root, leaf = 0, sp = 0;
-  while (w != kNone || leaf) {
-    while (!(w & kLeafBit) && w != kNone) {
-      const float4* q = reinterpret_cast<const float4*>(S.nodes4 + w);
-      float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
-      uint4 Cw = reinterpret_cast<const uint4*>(q)[6];
-      if (COUNT) tally.nodes += 2;  // counted in 64-B units
-      float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
-      float k0, k1, k2, k3;  // entry distance, +inf when the child is missed
-      if (!zl) {
-        auto slab = [&](float lx, float hx, float ly, float hy, float lz, float hz) {
-          float a = fmaf(lx, ix, ox), b = fmaf(hx, ix, ox);
-          float c = fmaf(ly, iy, oy), d = fmaf(hy, iy, oy);
-          float e = fmaf(lz, iz, oz), f = fmaf(hz, iz, oz);
-          float tn = fmaxf(fmaxf(fminf(a, b), fminf(c, d)), fmaxf(fminf(e, f), -1e-6f));
-          float tf = fminf(fminf(fmaxf(a, b), fmaxf(c, d)), fminf(fmaxf(e, f), tmax_lim));
-          return tn <= tf ? tn : kInfinity;
-        };
-        k0 = slab(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x);
-        k1 = slab(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y);
-        k2 = slab(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z);
-        k3 = slab(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w);
-      } else {
-        f3 s = r.start;
-        auto inside = [&](float lx, float hx, float ly, float hy, float lz, float hz) {
-          return s.x >= lx && s.x <= hx && s.y >= ly && s.y <= hy && s.z >= lz && s.z <= hz ? 0.0f : kInfinity;
-        };
-        k0 = inside(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x);
-        k1 = inside(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y);
-        k2 = inside(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z);
-        k3 = inside(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w);
-      }
-      uint32_t c0 = Cw.x, c1 = Cw.y, c2 = Cw.z, c3 = Cw.w;
-      auto cx = [](float& ka, uint32_t& ca, float& kb, uint32_t& cb) {
-        bool sw = kb < ka;
-        float tk = sw ? kb : ka;
-        kb = sw ? ka : kb;
-        ka = tk;
-        uint32_t tc = sw ? cb : ca;
-        cb = sw ? ca : cb;
-        ca = tc;
-      };
-      cx(k0, c0, k1, c1);
-      cx(k2, c2, k3, c3);
-      cx(k0, c0, k2, c2);
-      cx(k1, c1, k3, c3);
-      cx(k1, c1, k2, c2);
-      if (k3 < kInfinity) st.push(sp, c3);
-      if (k2 < kInfinity) st.push(sp, c2);
-      if (k1 < kInfinity) st.push(sp, c1);
-      w = k0 < kInfinity ? c0 : st.pop(sp, kNone);
-      if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
-        leaf = w;
-        w = st.pop(sp, kNone);
-      }
-      if (__ballot(leaf == 0) == 0) break;
-    }
-    while (leaf) {
-      test_leaf<COUNT>(S, leaf, oi, r, zl, h, tally);
-      leaf = 0;
-      if (w & kLeafBit) {
-        leaf = w;
-        w = st.pop(sp, kNone);
-      }
-    }
-  }
-}
-
 // Conservative segment-vs-box cull for analytic objects (not a reference
 // test): the slab interval uses v_rcp and the same t margins as the BVH
 // traversal, against a box padded on the host (fs_scene.cpp). A segment that
@@ -1498,11 +777,10 @@ struct PhaseAcc {};
 // SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
 // resume it in a later call with the same ray: objects before the parked one
 // are skipped on resume (already processed), the rest follow in order.
-template <bool COUNT, bool WW = false, bool WIDE = false, bool TEX = false, bool SUSP = false>
+template <bool COUNT, bool TEX = false, bool SUSP = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
-                                                PhaseAcc& pa, uint32_t* __restrict__ ovf = nullptr,
-                                                WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
+                                                PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
                                                 bool* parked = nullptr) {
   bool resuming = SUSP && ws->oi >= 0;
   if (!resuming) {
@@ -1543,12 +821,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         if (resume_here) resuming = false;
         if (park) continue;
       } else if (visit) {
-        if (WIDE && o->i3 >= 0)
-          traverse4_ww<COUNT>(S, (uint32_t)o->i3, (int32_t)oi, r, zl, h, LaneStack{stk, ovf}, tally);
-        else if (WW)
-          traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
-        else
-          traverse_min<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally);
+        traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
       }
       // MeshObject::Trace writes surface_texcoords only when the mesh has
       // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
@@ -1626,253 +899,6 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     *parked = park;
   }
 }
-
-// dense: one thread per slot in slot order (coherent, no list) while most
-// paths are alive; otherwise the compacted list `cur`.
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock) void wf_extend(DevScene S, WfState W, uint32_t cur, uint32_t dense, uint32_t spp,
-                                                     DevCounters* __restrict__ counters) {
-  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t slot;
-  if (dense) {
-    slot = i;
-    if (W.samples[slot] >= spp) return;
-  } else {
-    if (i >= W.count[cur]) return;
-    slot = (cur ? W.list1 : W.list0)[i];
-  }
-  Ray r = wf_load_ray(W, slot);
-  MinHit h;
-  Tally<COUNT> tally;
-  PhaseAcc pa;
-  scene_trace_min<COUNT>(S, r, h, stk_all + threadIdx.x, tally, pa);
-  WfHit o;
-  o.t = h.t;
-  o.u = h.u;
-  o.v = h.v;
-  o.obj = h.obj;
-  o.prim = h.prim;
-  o.point = h.point;
-  o.pad0 = o.pad1 = 0;
-  W.hit[slot] = o;
-  if (COUNT) {
-    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
-  }
-}
-
-// Pixel of a slot: the same 8x8 micro-tile walk as render_kernel.
-__device__ __forceinline__ bool slot_pixel(const Launch& P, const DevFrame& F, uint32_t slot, uint32_t& x,
-                                           uint32_t& y) {
-  const uint32_t micro_per_side = P.tile_size / 8;
-  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
-  const uint32_t blk = slot / kBlock, lane = slot % kBlock;
-  const uint32_t owned = blk / micro_per_tile, micro = blk % micro_per_tile;
-  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
-  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  x = tx * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
-  y = ty * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
-  return x < F.width && y < F.height;
-}
-
-__device__ __forceinline__ void wf_new_sample(const DevCamera& C, const Launch& P, const WfState& W, uint32_t slot,
-                                              uint32_t pix, uint32_t s, uint32_t width) {
-  uint64_t rng = pixel_seed(pix, (uint64_t)P.sample_base + s, P.seed);
-  Ray r = camera_ray(C, (float)(pix % width), (float)(pix / width), rng);
-  wf_store_ray(W, slot, r);
-  W.rng[slot] = rng;
-  W.path[slot] = make_uint4(0, 0xFFFFFFFFu, 0, 0);  // depth 0, top -1
-  W.p0[slot] = make_float4(0, 0, 0, 0);
-  W.lp0[slot] = make_float2(0, 0);
-}
-
-// Appends `keep` lanes' slots to list `nxt` with one atomic per wave.
-__device__ __forceinline__ void wf_append(const WfState& W, uint32_t nxt, bool keep, uint32_t slot,
-                                          bool write_list = true) {
-  uint64_t mask = __ballot(keep);
-  if (!mask) return;
-  uint32_t lane = threadIdx.x & 63u;
-  uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-  int leader = __ffsll((unsigned long long)mask) - 1;
-  uint32_t base = 0;
-  if ((int)lane == leader) base = atomicAdd(&W.count[nxt], (uint32_t)__popcll(mask));
-  base = __shfl(base, leader);
-  if (keep && write_list) (nxt ? W.list1 : W.list0)[base + rank] = slot;
-}
-
-// Compacts the live slots into list 0 (slot order within each wave).
-__global__ __launch_bounds__(kBlock) void wf_compact(WfState W, uint32_t slots, uint32_t spp) {
-  uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-  bool keep = slot < slots && W.samples[slot] < spp;
-  wf_append(W, 0, keep, slot);
-}
-
-__global__ __launch_bounds__(kBlock) void wf_begin(DevCamera C, DevFrame F, Launch P, WfState W) {
-  uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t x, y;
-  bool keep = slot_pixel(P, F, slot, x, y) && P.spp > 0;
-  W.samples[slot] = P.spp;  // invalid slots stay "done"
-  if (keep) {
-    uint32_t pix = y * F.width + x;
-    W.pixel[slot] = pix;
-    W.acc[slot] = make_float4(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2],
-                              __uint_as_float(F.count[pix]));
-    W.samples[slot] = 0;
-    W.aov[slot] = make_float4(0, 0, 0, 0);
-    W.aov_id[slot] = 0;
-    wf_new_sample(C, P, W, slot, pix, 0, F.width);
-  }
-  wf_append(W, 0, keep, slot);
-}
-
-template <bool COUNT>
-__global__ __launch_bounds__(kBlock) void wf_shade(DevScene S, DevCamera C, DevFrame F, Launch P, WfState W,
-                                                    uint32_t cur, uint32_t dense, DevCounters* __restrict__ counters) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  bool keep = false;
-  uint32_t slot = 0;
-  bool live;
-  if (dense) {
-    slot = i;
-    live = W.samples[slot] < P.spp;
-  } else {
-    live = i < W.count[cur];
-    if (live) slot = (cur ? W.list1 : W.list0)[i];
-  }
-  if (live) {
-    Ray r = wf_load_ray(W, slot);
-    WfHit h = W.hit[slot];
-    uint4 path = W.path[slot];
-    uint32_t depth = path.x, mats_lo = path.z, mats_hi = path.w;
-    int top = (int)path.y;
-    uint64_t rng = W.rng[slot];
-    float2* lvl = W.lvl + (size_t)slot * kMaxDepth;
-    bool done = false;
-    f3 L = mk3(0, 0, 0);
-    if (h.obj < 0) {  // engine.cpp:88-102
-      if (depth == 1) W.lp0[slot] = make_float2(r.stop.y, r.stop.z), W.p0[slot].w = r.stop.x;
-      L = mk3(S.sky_r, S.sky_g, S.sky_b);
-      if (depth == 0) {
-        f3 nd = normalize(r.dir);
-        W.aov[slot] = make_float4(nd.x, nd.y, nd.z, C.z_far);
-        W.aov_id[slot] = S.sky_id;
-      }
-      done = true;
-    } else {
-      // Rebuild the hit exactly as the object tests produced it.
-      const DevObject* __restrict__ o = S.objects + h.obj;
-      const float* d = o->d;
-      f3 p = h.point ? r.start : r.start + r.dir * h.t;
-      f3 n;
-      if (o->kind == FS_OBJ_MESH) {
-        TriData T = load_tri(S.tris, h.prim);
-        n = xyz(T.pl);
-        if (o->i1) {  // mesh.cpp:289-298
-          const float4* nq = S.tri_normals + 3 * (size_t)h.prim;
-          float4 a = nq[0], b = nq[1], c = nq[2];
-          f3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(b.x, b.y, b.z), n2 = mk3(c.x, c.y, c.z);
-          n = n0 + (n1 - n0) * h.u + (n2 - n0) * h.v;
-        }
-      } else if (o->kind == FS_OBJ_SPHERE) {
-        n = normalize(p - mk3(d[0], d[1], d[2]));
-      } else if (o->kind == FS_OBJ_CUBOID) {
-        n = mk3(d[4 * h.prim], d[4 * h.prim + 1], d[4 * h.prim + 2]);
-      } else {
-        n = mk3(d[0], d[1], d[2]);
-      }
-      f4 cp = plane_np(n, p);  // scene.cpp:238-247
-      if (plane_dist(cp, r.start) < 0.0f) n = n * (float)-1.0;
-      if (depth == 1) W.lp0[slot] = make_float2(p.y, p.z), W.p0[slot].w = p.x;
-      int32_t mi = o->mat;
-      const fs_material& m = S.materials[mi];
-      int32_t kind = m.kind;
-      f3 view = normalize(p - r.start);
-      f3 refl = mat_reflection(S, m, view, n, rng);
-      float c = fmaxf(0.0f, dot(n, refl));
-      float ds = 0.0f;
-      if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {
-        f3 hv = normalize(view * (float)-1.0 + refl);
-        ds = pow50(dot(hv, n));
-      }
-      lvl[depth] = make_float2(c, ds);
-      if (depth < 4)
-        mats_lo |= (uint32_t)mi << (8 * depth);
-      else
-        mats_hi |= (uint32_t)mi << (8 * (depth - 4));
-      top = (int)depth;
-      if (depth == 0) {
-        W.p0[slot] = make_float4(p.x, p.y, p.z, 0.0f);
-        W.aov[slot] = make_float4(n.x, n.y, n.z, length(r.start - p));
-        W.aov_id[slot] = m.id;
-      }
-      bool use = mat_will_use(m, refl, n);
-      Ray nr;  // engine.cpp:120-127
-      nr.start = p;
-      nr.stop = p + refl * C.z_far;
-      nr.dir = nr.stop - nr.start;
-      f3 off = refl * kStepOffset;
-      nr.start = nr.start + off;
-      nr.dir = nr.dir - off;
-      if (!use) {
-        done = true;
-      } else {
-        depth++;
-        if (depth >= kMaxDepth) {  // engine.cpp:62-64
-          done = true;
-        } else if (C.fast_render && depth > 1) {  // engine.cpp:68-70
-          L = mk3(1, 1, 1);
-          done = true;
-        } else {
-          wf_store_ray(W, slot, nr);
-        }
-      }
-    }
-    if (done) {
-      float4 pa = W.p0[slot];
-      float2 pb = W.lp0[slot];
-      L = unwind(S, L, top, mats_lo, mats_hi, lvl, mk3(pa.x, pa.y, pa.z), mk3(pa.w, pb.x, pb.y), rng, 1);
-      float4 acc = W.acc[slot];
-      uint32_t n = __float_as_uint(acc.w);
-      f3 np = mk3(acc.x, acc.y, acc.z) * (float)n + L;
-      float dv = (float)(++n);
-      f3 mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-      uint32_t s = W.samples[slot] + 1;
-      W.samples[slot] = s;
-      if (s < P.spp) {
-        W.acc[slot] = make_float4(mean.x, mean.y, mean.z, __uint_as_float(n));
-        wf_new_sample(C, P, W, slot, W.pixel[slot], s, F.width);
-        keep = true;
-      } else {  // all samples of this pixel done: write the DisplayFrame
-        size_t pix = W.pixel[slot];
-        F.color[3 * pix] = mean.x;
-        F.color[3 * pix + 1] = mean.y;
-        F.color[3 * pix + 2] = mean.z;
-        F.count[pix] = n;
-        F.display[3 * pix] = gamma8(mean.x);
-        F.display[3 * pix + 1] = gamma8(mean.y);
-        F.display[3 * pix + 2] = gamma8(mean.z);
-        float4 av = W.aov[slot];
-        F.normal[3 * pix] = av.x;
-        F.normal[3 * pix + 1] = av.y;
-        F.normal[3 * pix + 2] = av.z;
-        F.depth[pix] = av.w;
-        F.material[pix] = W.aov_id[slot];
-      }
-    } else {
-      W.path[slot] = make_uint4(depth, (uint32_t)top, mats_lo, mats_hi);
-      W.rng[slot] = rng;
-      keep = true;
-    }
-    if (COUNT) {
-      atomicAdd(&counters->segments, 1ull);
-      if (done) atomicAdd(&counters->samples, 1ull);
-    }
-  }
-  wf_append(W, cur ^ 1u, keep, slot, !dense);
-}
-
 
 // ---- textures (material.cpp:108-126, intersect.cpp:769-784) -------------
 // planar_map_texcoords
@@ -2028,12 +1054,10 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool WW = false, bool WIDE = false, bool TEX = false, bool POOL = false,
-          bool SUSP = false>
+template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
-                                                                     uint32_t* __restrict__ ovf_all,
                                                                      float4* __restrict__ tex_all,
                                                                      float* __restrict__ rad_all,
                                                                      DevCounters* __restrict__ counters) {
@@ -2045,7 +1069,6 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   float2* lvl = lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
   float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
-  uint32_t* ovf = ovf_all + (size_t)blockIdx.x * (kStackOverflow * kBlock) + lane;
   float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   uint32_t x0, y0;  // the wave's 8x8 pixel micro-tile
@@ -2088,18 +1111,11 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   const bool last_group = group + 1 == P.groups;
   uint32_t x = x0 + (lane & 7), y = y0 + (lane >> 3);
   const bool own_valid = x < F.width && y < F.height;
-  if (!POOL && !own_valid) return;
-  if (POOL && (x0 >= F.width || y0 >= F.height)) return;  // whole micro-tile outside the frame
+  if (x0 >= F.width || y0 >= F.height) return;  // whole micro-tile outside the frame
   uint32_t pix = y * F.width + x;
-  f3 mean = mk3(0, 0, 0);
-  uint32_t n = 0;
-  if (!POOL) {
-    mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
-    n = F.count[pix];
-  }
   Tally<COUNT> tally;
   uint32_t segments = 0;
-  // POOL: the wave's kBlock x spp (pixel, sample) tasks are taken in
+  // The wave's kBlock x spp (pixel, sample) tasks are taken in
   // sample-major order from a wave-uniform counter by whichever lane is
   // free; each sample's radiance goes to a scratch row and every pixel folds
   // its samples in order at the end (same running-mean rounding).
@@ -2134,9 +1150,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   } while (0)
 #endif
   for (;;) {
-    if (!POOL && s >= P.spp) break;
     FS_PHASE(0);
-    if (POOL) {
+    {
       const uint64_t m = __ballot(fresh);
       if (fresh) {
         uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -2175,7 +1190,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
       const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
-      scene_trace_min<COUNT, WW, WIDE, TEX, SUSP>(S, r, h, stk, tally, pa, ovf, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
@@ -2204,7 +1219,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       }
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, WW, WIDE, TEX, SUSP>(S, r, h, stk, tally, pa, ovf, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
 #endif
       FS_PHASE(2);
       if (SUSP && parked) {
@@ -2217,7 +1232,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           sphere_tc(normalize(r.stop - r.start), tu, tv);
           L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
         }
-        if (depth == 0 && (!POOL || (last_group && s == P.spp - 1))) {  // the last sample's AOVs remain
+        if (depth == 0 && last_group && s == P.spp - 1) {  // the last sample's AOVs remain
           f3 nd = normalize(r.dir);
           at_byte(F.normal, pix * 12u)[0] = nd.x;
           at_byte(F.normal, pix * 12u)[1] = nd.y;
@@ -2253,7 +1268,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           mats_hi |= (uint32_t)mi << (8 * (depth - 4));
         top = (int)depth;
         if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
-        if (depth == 0 && (!POOL || (last_group && s == P.spp - 1))) {
+        if (depth == 0 && last_group && s == P.spp - 1) {
           at_byte(F.normal, pix * 12u)[0] = nn.x;
           at_byte(F.normal, pix * 12u)[1] = nn.y;
           at_byte(F.normal, pix * 12u)[2] = nn.z;
@@ -2284,17 +1299,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX>(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      if (POOL) {
-        const uint32_t o = s * kBlock + task_lp;
-        rad[o] = L.x;
-        rad[kChunk * kBlock + o] = L.y;
-        rad[2 * kChunk * kBlock + o] = L.z;
-      } else {
-        f3 np = mean * (float)n + L;
-        float dv = (float)(++n);
-        mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-        s++;
-      }
+      const uint32_t o = s * kBlock + task_lp;
+      rad[o] = L.x;
+      rad[kChunk * kBlock + o] = L.y;
+      rad[2 * kChunk * kBlock + o] = L.z;
       fresh = true;
     }
     FS_PHASE(4);
@@ -2312,31 +1320,27 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   atomicAdd(&counters->phase[13], (unsigned long long)tally.lane_leaves);
 #endif
 #undef FS_PHASE
-  if (POOL) {
-    __syncthreads();  // the wave's radiance rows are complete and visible
-    if (!own_valid) return;
-    if (P.groups > 1) {  // fold_groups folds every group's rows in sample order
-      if (COUNT) {
-        atomicAdd(&counters->samples, (unsigned long long)P.spp);
-        atomicAdd(&counters->segments, (unsigned long long)segments);
-        atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-        atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-        atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
-      }
-      return;
-    }
-    x = x0 + (lane & 7);
-    y = y0 + (lane >> 3);
-    pix = y * F.width + x;
-    mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
-    n = F.count[pix];
-    for (uint32_t k = 0; k < P.spp; k++) {  // frame.cpp:53-63, samples in order
-      const uint32_t o = k * kBlock + lane;
-      f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
-      f3 np = mean * (float)n + L;
-      float dv = (float)(++n);
-      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-    }
+  __syncthreads();  // the wave's radiance rows are complete and visible
+  if (COUNT) {  // every lane's work; samples once per in-frame pixel
+    if (own_valid) atomicAdd(&counters->samples, (unsigned long long)P.spp);
+    atomicAdd(&counters->segments, (unsigned long long)segments);
+    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+  }
+  if (!own_valid) return;
+  if (P.groups > 1) return;  // fold_groups folds every group's rows in sample order
+  x = x0 + (lane & 7);
+  y = y0 + (lane >> 3);
+  pix = y * F.width + x;
+  f3 mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
+  uint32_t n = F.count[pix];
+  for (uint32_t k = 0; k < P.spp; k++) {  // frame.cpp:53-63, samples in order
+    const uint32_t o = k * kBlock + lane;
+    f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
+    f3 np = mean * (float)n + L;
+    float dv = (float)(++n);
+    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
   }
   F.color[3 * (size_t)pix] = mean.x;
   F.color[3 * (size_t)pix + 1] = mean.y;
@@ -2345,13 +1349,6 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   F.display[3 * (size_t)pix] = gamma8(mean.x);
   F.display[3 * (size_t)pix + 1] = gamma8(mean.y);
   F.display[3 * (size_t)pix + 2] = gamma8(mean.z);
-  if (COUNT) {
-    atomicAdd(&counters->samples, (unsigned long long)P.spp);
-    atomicAdd(&counters->segments, (unsigned long long)segments);
-    atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-    atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-    atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
-  }
 }
 
 // Folds the radiance rows of a launch with P.groups > 1 into the frame:
@@ -2408,7 +1405,7 @@ __global__ __launch_bounds__(kBlock) void trace_range_kernel(DevScene S, DevCame
   MinHit h;
   Tally<false> tally;
   PhaseAcc pa;
-  scene_trace_min<false, true>(S, r, h, stk_all + threadIdx.x, tally, pa);
+  scene_trace_min<false>(S, r, h, stk_all + threadIdx.x, tally, pa);
   float d = C.z_far;
   if (h.obj >= 0) {
     f3 p = h.point ? r.start : r.start + r.dir * h.t;
@@ -2524,10 +1521,11 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
+  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
       pack_recv, range_io;
+  fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
-  bool has_parking = false;  // a mesh of >= kParkMinTris triangles: the SUSP schedule
+  bool has_parking = false;  // a mesh of >= park_min_tris triangles: the PARKED schedule
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
   std::vector<uint32_t> tile_order_host;  // the device tile_order buffer holds this order of ...
   uint64_t tile_order_key[3] = {0, 0, 0};  // ... the tile set (offset, stride, owned; width, height) it was built for
@@ -2542,9 +1540,7 @@ struct fs_context {
   float last_ms = 0.0f;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  DevBuf wf;              // wavefront path state (slots x ~250 B)
-  uint32_t wf_slots = 0;
-  uint32_t* host_count = nullptr;  // pinned
+  DevBuf rows;  // per-lane scratch rows of the lean kernel (LeanRows)
 };
 
 struct fs_frame {
@@ -2616,58 +1612,34 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
   return b;
 }
 
-// Carves the wavefront state for `slots` paths out of one allocation.
-// The lean kernels use only the shading rows (lvl), the Fog anchors (p0),
-// the BVH4 overflow stack (ovf, lean_bvh4 only), texel rows and radiance rows.
-int wf_state(fs_context* ctx, uint32_t slots, dev::WfState* W, bool tex_rows = false, bool lean = false,
-             bool ovf_rows = true) {
-  size_t per = lean ? 8 * kMaxDepth + 32 + (ovf_rows ? 4 * kStackOverflow : 0) + (tex_rows ? 16 * kMaxDepth : 0) +
-                          12 * kChunk
-                    : 4 + 16 + 16 + 4 + sizeof(dev::WfHit) + 8 + 16 + 32 + 8 + 8 * kMaxDepth + 16 + 4 + 16 + 8 + 4 +
-                          4 + 4 * kStackOverflow + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
-  size_t bytes = (size_t)slots * per + 64 * 32 + 256 * 24;  // + alignment of each array
-  if (ctx->wf.bytes < bytes) {
-    int rc = ensure(&ctx->wf, bytes);
+// Per-lane scratch rows of the lean kernel, carved out of one allocation:
+// the shading scalars (lvl), the Fog anchors, texel rows (textured scenes)
+// and the radiance rows of the pooled samples.
+struct LeanRows {
+  float2* lvl = nullptr;
+  float4* anchor = nullptr;
+  float4* tex = nullptr;
+  float* rad = nullptr;
+};
+int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows) {
+  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
+  const size_t bytes = (size_t)slots * per + 4 * 256;  // + alignment of each array
+  if (ctx->rows.bytes < bytes) {
+    int rc = ensure(&ctx->rows, bytes);
     if (rc) return rc;
   }
-  char* p = (char*)ctx->wf.p;
+  char* p = (char*)ctx->rows.p;
   auto take = [&](size_t n) {
     char* q = p;
     p += (n + 255) & ~(size_t)255;
     return q;
   };
-  *W = dev::WfState{};
-  W->count = (uint32_t*)take(64);
-  if (lean) {
-    W->p0 = (float4*)take(32ull * slots);
-    W->lvl = (float2*)take(8ull * kMaxDepth * slots);
-    W->ovf = ovf_rows ? (uint32_t*)take(4ull * kStackOverflow * slots) : nullptr;
-    W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
-    W->rad = (float*)take(12ull * kChunk * slots);
-    if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
-    return FS_OK;
-  }
-  W->pixel = (uint32_t*)take(4ull * slots);
-  W->ray0 = (float4*)take(16ull * slots);
-  W->ray1 = (float4*)take(16ull * slots);
-  W->ray2 = (float*)take(4ull * slots);
-  W->hit = (dev::WfHit*)take(sizeof(dev::WfHit) * (size_t)slots);
-  W->rng = (uint64_t*)take(8ull * slots);
-  W->path = (uint4*)take(16ull * slots);
-  W->p0 = (float4*)take(32ull * slots);  // wavefront: 1 float4/slot; lean megakernel: 2
-  W->lp0 = (float2*)take(8ull * slots);
+  *W = LeanRows{};
+  W->anchor = (float4*)take(32ull * slots);
   W->lvl = (float2*)take(8ull * kMaxDepth * slots);
-  W->acc = (float4*)take(16ull * slots);
-  W->samples = (uint32_t*)take(4ull * slots);
-  W->aov = (float4*)take(16ull * slots);
-  W->aov_id = (uint64_t*)take(8ull * slots);
-  W->list0 = (uint32_t*)take(4ull * slots);
-  W->list1 = (uint32_t*)take(4ull * slots);
-  W->ovf = (uint32_t*)take(4ull * kStackOverflow * slots);
   W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
   W->rad = (float*)take(12ull * kChunk * slots);
-  if ((size_t)(p - (char*)ctx->wf.p) > ctx->wf.bytes) return fail(FS_ERR_NOMEM, "wavefront state overflow");
-  if (!ctx->host_count) FS_HIP(hipHostMalloc((void**)&ctx->host_count, 16, hipHostMallocDefault));
+  if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
   return FS_OK;
 }
 
@@ -2733,21 +1705,15 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
 
-enum class KernelMode { kAuto, kLean, kLeanSusp, kLeanNoPool, kLeanBvh4, kLeanIfIf, kRegen, kLockstep, kWavefront };
-
-KernelMode kernel_mode() {
-  const char* e = std::getenv("FS_KERNEL");
-  if (!e || !*e) return KernelMode::kAuto;
-  std::string m(e);
-  if (m == "regen") return KernelMode::kRegen;
-  if (m == "lean_ifif") return KernelMode::kLeanIfIf;
-  if (m == "lean_bvh4") return KernelMode::kLeanBvh4;
-  if (m == "lean_nopool") return KernelMode::kLeanNoPool;
-  if (m == "lean_susp") return KernelMode::kLeanSusp;
-  if (m == "lean") return KernelMode::kLean;
-  if (m == "lockstep") return KernelMode::kLockstep;
-  if (m == "wavefront") return KernelMode::kWavefront;
-  return KernelMode::kAuto;
+bool valid_options(const fs_options* o, std::string* why) {
+  if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_PARKED) *why = "unknown schedule";
+  else if (o->samples_per_block < 1 || o->samples_per_block > kChunk) *why = "samples_per_block must be 1..64";
+  else if (o->xcd_bands > 2) *why = "xcd_bands must be 0, 1 or 2";
+  else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..127";
+  else if (o->bvh_bins < 2 || o->bvh_bins > 64) *why = "bvh_bins must be 2..64";
+  else if (o->node_layout > FS_NODE_LAYOUT_PAIRS) *why = "unknown node_layout";
+  else return true;
+  return false;
 }
 
 }  // namespace
@@ -2773,6 +1739,7 @@ int fs_create(int device, fs_context** out) {
   if (device < 0 || device >= n) return fail(FS_ERR_INVALID, "device index out of range");
   std::unique_ptr<fs_context> ctx(new fs_context());
   ctx->device = device;
+  fs_options_default(&ctx->opt);
   FS_HIP(hipSetDevice(device));
   FS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   FS_HIP(hipEventCreate(&ctx->ev0));
@@ -2789,12 +1756,11 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order})
     b->release();
-  ctx->wf.release();
-  if (ctx->host_count) (void)hipHostFree(ctx->host_count);
+  ctx->rows.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2802,10 +1768,41 @@ int fs_destroy(fs_context* ctx) {
   return FS_OK;
 }
 
-int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) {
-  const char* e = std::getenv("FS_GPU_BVH");
-  return fs_upload_scene_ex(ctx, desc, (e && std::atoi(e)) ? FS_UPLOAD_GPU_BVH : 0u);
+int fs_options_default(fs_options* o) {
+  if (!o) return fail(FS_ERR_INVALID, "null options");
+  *o = fs_options{};
+  o->schedule = FS_SCHEDULE_AUTO;
+  o->park_lanes = 10;  // C4: 8-10 best at 6 waves per SIMD
+  o->park_min_tris = kParkMinTris;
+  o->samples_per_block = kChunk;
+  o->groups = 0;
+  o->group_major = 0;
+  o->tile_order = 1;
+  o->xcd_bands = 2;
+  o->gpu_bvh_min_tris = kGpuBvhMinTris;
+  o->bvh_leaf = 2;
+  o->bvh_bins = 16;
+  o->bvh_threads = 0;
+  o->node_layout = FS_NODE_LAYOUT_DEPTH_FIRST;
+  o->build_log = 0;
+  return FS_OK;
 }
+
+int fs_set_options(fs_context* ctx, const fs_options* opt) {
+  if (!ctx || !opt) return fail(FS_ERR_INVALID, "null argument");
+  std::string why;
+  if (!valid_options(opt, &why)) return fail(FS_ERR_INVALID, "fs_set_options: " + why);
+  ctx->opt = *opt;
+  return FS_OK;
+}
+
+int fs_get_options(fs_context* ctx, fs_options* out) {
+  if (!ctx || !out) return fail(FS_ERR_INVALID, "null argument");
+  *out = ctx->opt;
+  return FS_OK;
+}
+
+int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc) { return fs_upload_scene_ex(ctx, desc, 0u); }
 
 int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flags) {
   if (!ctx) return fail(FS_ERR_INVALID, "null context");
@@ -2817,12 +1814,9 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   // build than the level-synchronous launches. FS_GPU_BVH_MIN_TRIS lowers
   // the threshold (tests), never below the device builder's minimum.
   uint32_t gpu_min = 0;
-  if (flags & FS_UPLOAD_GPU_BVH) {
-    const char* m = std::getenv("FS_GPU_BVH_MIN_TRIS");
-    gpu_min = m ? (uint32_t)std::strtoul(m, nullptr, 10) : kGpuBvhMinTris;
-    gpu_min = std::max(gpu_min, kGpuBvhFloor);
-  }
-  int rc = prepare_scene(desc, &P, &err, gpu_min);
+  if (flags & FS_UPLOAD_GPU_BVH) gpu_min = std::max(ctx->opt.gpu_bvh_min_tris, kGpuBvhFloor);
+  const BuildOptions bo = BuildOptions::from(&ctx->opt);
+  int rc = prepare_scene(desc, &P, &err, bo, gpu_min);
   if (rc) return fail(rc, err);
   if (P.materials.size() > 255) return fail(FS_ERR_INVALID, "at most 255 materials are supported");
   if ((rc = set_device(ctx))) return rc;
@@ -2832,7 +1826,6 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   if ((rc = upload(ctx, &ctx->nodes, P.nodes.data(), P.nodes.size() * sizeof(BvhNode),
                    (size_t)P.deferred_nodes * sizeof(BvhNode))))
     return rc;
-  if ((rc = upload(ctx, &ctx->nodes4, P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node)))) return rc;
   if ((rc = upload(ctx, &ctx->tris, P.tris.data(), P.tris.size() * sizeof(DevTri),
                    (size_t)P.deferred_tris * sizeof(DevTri))))
     return rc;
@@ -2859,7 +1852,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
     job.normals = D.normals.empty() ? nullptr : D.normals.data();
     job.tex = D.tex.empty() ? nullptr : D.tex.data();
     job.num_tris = D.num_tris;
-    job.leaf = bvh_leaf_target();
+    job.leaf = bo.leaf;
+    job.log = bo.log;
     job.node_base = D.node_base;
     job.tri_base = D.tri_base;
     GpuBvhResult res;
@@ -2869,7 +1863,7 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
     P.max_depth = std::max(P.max_depth, res.max_depth);
     ctx->gpu_bvh_ms += res.build_ms;
     ctx->gpu_bvh_nodes += res.nodes_used;
-    if (std::getenv("FS_BUILD_LOG"))
+    if (bo.log)
       std::fprintf(stderr, "[fs build] mesh %u: %u tris, device bvh %.1f ms (%u levels, %u nodes, depth %u)\n", D.mesh,
                    D.num_tris, res.build_ms, res.levels, res.nodes_used, res.max_depth);
     D = DeferredMesh();  // release the host copies
@@ -2877,7 +1871,6 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   DevScene& S = ctx->scene;
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
-  S.nodes4 = (const Bvh4Node*)ctx->nodes4.p;
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
@@ -2919,7 +1912,7 @@ int fs_scene_stats(fs_context* ctx, double* build_ms, double* upload_ms, uint64_
   if (num_triangles) *num_triangles = ctx->host.tris.size() + ctx->gpu_bvh_tris;
   if (num_nodes) *num_nodes = ctx->host.nodes.size() + ctx->gpu_bvh_nodes;
   if (device_bytes)
-    *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->nodes4.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
+    *device_bytes = ctx->objects.bytes + ctx->nodes.bytes + ctx->tris.bytes + ctx->tri_normals.bytes +
                      ctx->materials.bytes + ctx->table.bytes;
   return FS_OK;
 }
@@ -3010,117 +2003,49 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_offset = params->tile_offset;
   L.tile_stride = stride;
   L.seed = params->seed;
-  L.susp_thr = std::getenv("FS_SUSP_THR") ? (uint32_t)std::atoi(std::getenv("FS_SUSP_THR")) : 10u;  // C4: 8-10 best at 6 waves, 10-12 at 5
-  // XCD placement (FS_XCD_BANDS): 0 dispatch order, 1 one band per XCD (C4 -25 %:
-  // the bands are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
-  L.xcd_bands = std::getenv("FS_XCD_BANDS") ? (uint32_t)std::atoi(std::getenv("FS_XCD_BANDS")) : 2u;
+  const fs_options& O = ctx->opt;
+  L.susp_thr = O.park_lanes;
+  // XCD placement: 0 dispatch order, 1 one band per XCD (C4 -25 %: the bands
+  // are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
+  L.xcd_bands = O.xcd_bands;
   uint32_t owned = params->tile_offset < tiles ? (tiles - params->tile_offset + stride - 1) / stride : 0;
   uint64_t blocks = (uint64_t)owned * (ts / 8) * (ts / 8);
   DevCamera C = camera_basis(camera, params->width, params->height);
   DevFrame F = frame_view(frame);
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
-  // Long renders are split into launches of at most `chunk` samples per
-  // pixel; the running mean lives in the frame, so the result is identical.
-  // Samples per block: kChunk, or fewer by FS_CHUNK_RT (A/B). The kernel
-  // takes any per-block count up to kChunk (the radiance rows keep the
-  // kChunk stride).
-  uint32_t chunk = kChunk;
-  if (const char* e = std::getenv("FS_CHUNK_RT")) chunk = std::min<uint32_t>(kChunk, std::max(1, std::atoi(e)));
-  // Kernel schedule (FS_KERNEL, read per call for A/B runs; every schedule
-  // produces identical frames): "lean" path-regeneration megakernel with the
-  // unwind scratch in HBM rows, while-while traversal and the wave's
-  // (pixel, sample) tasks pooled across lanes; "lean_susp" the same with walks
-  // of large meshes parked when few lanes still walk (the default when the
-  // scene has a mesh of >= kParkMinTris triangles, else "lean");
-  // "lean_nopool" one pixel per lane;
-  // "lean_bvh4" with 4-wide nodes for scenes uploaded with FS_BVH4=1 (slower:
-  // more VALU per step); "lean_ifif" the single-loop traversal; "regen" with the unwind
-  // stack in VGPRs; "lockstep" one sample per lane in lockstep; "wavefront"
-  // extend/shade kernels over a compacted path queue.
-  KernelMode mode = kernel_mode();
-  if (mode == KernelMode::kAuto)
-    mode = ctx->has_parking && !ctx->has_textures ? KernelMode::kLeanSusp : KernelMode::kLean;
-  if (ctx->has_textures && mode != KernelMode::kLean && mode != KernelMode::kLeanSusp && mode != KernelMode::kLeanNoPool &&
-      mode != KernelMode::kLeanBvh4 &&
-      mode != KernelMode::kLeanIfIf)
-    return fail(FS_ERR_INVALID, "textured scenes need the default (lean) kernel schedule");
+  // Long renders are split into launches of sample groups of `chunk` samples
+  // per pixel; the running mean lives in the frame, so the result is
+  // identical. The kernel takes any per-block count up to kChunk (the
+  // radiance rows keep the kChunk stride).
+  const uint32_t chunk = O.samples_per_block;
+  // Schedule (every schedule produces identical frames): LEAN, the
+  // path-regeneration megakernel with the unwind scratch in HBM rows,
+  // while-while traversal and the wave's (pixel, sample) tasks pooled across
+  // lanes; PARKED the same with walks of large meshes parked when few lanes
+  // still walk. AUTO: PARKED when the scene has a mesh of >= park_min_tris
+  // triangles and no texture (the textured instantiation has no parking).
+  const bool parked = O.schedule == FS_SCHEDULE_PARKED ||
+                      (O.schedule == FS_SCHEDULE_AUTO && ctx->has_parking && !ctx->has_textures);
+  if (parked && ctx->has_textures) return fail(FS_ERR_INVALID, "the PARKED schedule does not take textured scenes");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-  if (mode == KernelMode::kWavefront && blocks && params->spp) {
-    // Wavefront: begin -> (extend, shade)* until no path is alive.
-    dev::WfState W;
-    uint32_t slots = (uint32_t)(blocks * kBlock);
-    if ((rc = wf_state(ctx, slots, &W))) return rc;
-    L.sample_base = params->sample_base;
-    L.spp = params->spp;
-    FS_HIP(hipMemsetAsync(W.count, 0, 16, ctx->stream));
-    hipLaunchKernelGGL(dev::wf_begin, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, C, F, L, W);
-    FS_HIP(hipGetLastError());
-    auto ext = count ? dev::wf_extend<true> : dev::wf_extend<false>;
-    auto shd = count ? dev::wf_shade<true> : dev::wf_shade<false>;
-    DevCounters* dc = (DevCounters*)ctx->counters.p;
-    uint32_t grid = (uint32_t)blocks;
-    auto read_count = [&](uint32_t which, uint32_t* out) -> int {
-      FS_HIP(hipMemcpyAsync(ctx->host_count, W.count + which, 4, hipMemcpyDeviceToHost, ctx->stream));
-      FS_HIP(hipStreamSynchronize(ctx->stream));
-      *out = *ctx->host_count;
-      return FS_OK;
-    };
-    // Dense phase: every slot in slot order until fewer than half are alive.
-    uint32_t live = slots;
-    for (uint32_t it = 1;; it++) {
-      FS_HIP(hipMemsetAsync(W.count + 1, 0, 4, ctx->stream));
-      hipLaunchKernelGGL(ext, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, W, 0u, 1u, L.spp, dc);
-      hipLaunchKernelGGL(shd, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, W, 0u, 1u, dc);
-      FS_HIP(hipGetLastError());
-      if (it % 8 == 0) {
-        if ((rc = read_count(1, &live))) return rc;
-        if (live == 0 || live < slots / 2) break;
-      }
-    }
-    // Sparse phase: compacted lists (ballot + one atomic per wave).
-    uint32_t cur = 0;
-    if (live) {
-      FS_HIP(hipMemsetAsync(W.count, 0, 4, ctx->stream));
-      hipLaunchKernelGGL(dev::wf_compact, dim3(grid), dim3(kBlock), 0, ctx->stream, W, slots, L.spp);
-      FS_HIP(hipGetLastError());
-      if ((rc = read_count(0, &live))) return rc;
-    }
-    while (live) {
-      uint32_t g = (live + kBlock - 1) / kBlock;
-      FS_HIP(hipMemsetAsync(W.count + (cur ^ 1u), 0, 4, ctx->stream));
-      hipLaunchKernelGGL(ext, dim3(g), dim3(kBlock), 0, ctx->stream, ctx->scene, W, cur, 0u, L.spp, dc);
-      hipLaunchKernelGGL(shd, dim3(g), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, W, cur, 0u, dc);
-      FS_HIP(hipGetLastError());
-      cur ^= 1u;
-      if ((rc = read_count(cur, &live))) return rc;
-    }
-    FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
-    return FS_OK;
-  }
-  dev::WfState lean{};
-  const bool lean_mode = mode == KernelMode::kLean || mode == KernelMode::kLeanSusp ||
-                         mode == KernelMode::kLeanNoPool || mode == KernelMode::kLeanBvh4 ||
-                         mode == KernelMode::kLeanIfIf;
-  // Sample groups (pooled lean kernels only): a launch renders G runs of
-  // `chunk` samples as G x blocks blocks, then fold_groups folds them in
-  // order. G is sized so a launch holds >= kGroupTargetBlocks blocks (about
-  // 20 waves per wave slot of the chip), which makes the launch tail small
-  // and keeps the CUs full when a multi-GPU rank owns few tiles.
-  const bool pooled = lean_mode && (ctx->has_textures || mode == KernelMode::kLean || mode == KernelMode::kLeanSusp);
+  // Sample groups: a launch renders G runs of `chunk` samples as
+  // G x blocks blocks, then fold_groups folds them in order. G is sized so a
+  // launch holds >= kGroupTargetBlocks blocks (about 43 per wave slot of the
+  // chip), which makes the launch tail small and keeps the CUs full when a
+  // multi-GPU rank owns few tiles.
   const uint32_t full_chunks = params->spp / chunk;
   uint32_t G = 1;
-  if (pooled && blocks && full_chunks > 1) {
-    uint64_t want = (kGroupTargetBlocks + blocks - 1) / blocks;
-    if (const char* e = std::getenv("FS_GROUPS")) want = (uint64_t)std::max(1, std::atoi(e));
+  if (blocks && full_chunks > 1) {
+    uint64_t want = O.groups ? (uint64_t)O.groups : (kGroupTargetBlocks + blocks - 1) / blocks;
     want = std::min<uint64_t>(want, full_chunks);
     const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
     G = (full_chunks + nl - 1) / nl;                                   // balanced groups per launch
   }
   L.owned = owned;
   L.groups = 1;
-  L.group_major = std::getenv("FS_GROUP_ORDER") ? (uint32_t)std::atoi(std::getenv("FS_GROUP_ORDER")) : 0u;
+  L.group_major = O.group_major;
   L.tile_order = nullptr;
-  if (pooled && owned > 1 && !(std::getenv("FS_TILE_ORDER") && std::atoi(std::getenv("FS_TILE_ORDER")) == 0)) {
+  if (owned > 1 && O.tile_order) {
     // Longest jobs first: tiles nearer the image centre (where the scenes put
     // their geometry) are dispatched first, so the launch tail runs on cheap
     // edge tiles. Ties keep index order.
@@ -3148,10 +2073,18 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   }
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
-  if (lean_mode && blocks) {  // per-lane scratch rows (the wavefront state buffers)
-    if ((rc = wf_state(ctx, (uint32_t)(blocks * G * kBlock), &lean, ctx->has_textures, true,
-                       mode == KernelMode::kLeanBvh4)))
-      return rc;
+  LeanRows rows;
+  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures))) return rc;
+  // (names as rocprofv3 prints the uncounted instantiations, for fs_last_kernel)
+  auto lk = count ? dev::render_kernel_lean<true, 6, false, false> : dev::render_kernel_lean<false, FS_LEAN_WAVES, false, false>;
+  ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_LEAN_WAVES) ", false, false>";
+  if (ctx->has_textures) {  // textured scenes: the instantiation with texcoords + texel rows
+    lk = count ? dev::render_kernel_lean<true, 6, true, false> : dev::render_kernel_lean<false, 6, true, false>;
+    ctx->last_kernel = "render_kernel_lean<false, 6, true, false>";
+  } else if (parked) {
+    lk = count ? dev::render_kernel_lean<true, 6, false, true>
+               : dev::render_kernel_lean<false, FS_SUSP_WAVES, false, true>;
+    ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_SUSP_WAVES) ", false, true>";
   }
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
@@ -3160,44 +2093,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     done += L.groups * L.spp;
     ctx->last_launches++;
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
-    // (names as rocprofv3 prints the uncounted instantiations, for fs_last_kernel)
-    auto kern = count ? dev::render_kernel_regen<true, 4> : dev::render_kernel_regen<false, 4>;
-    ctx->last_kernel = "render_kernel_regen<false, 4>";
-    if (mode == KernelMode::kLockstep) {
-      kern = count ? dev::render_kernel<true> : dev::render_kernel<false>;
-      ctx->last_kernel = "render_kernel<false>";
-    }
-    if (lean_mode) {
-      // default: while-while BVH2 traversal, pooled (pixel, sample) tasks
-      auto lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true>
-                      : dev::render_kernel_lean<false, FS_LEAN_WAVES, true, false, false, true>;
-      ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, true, false>";
-      if (ctx->has_textures) {  // textured scenes: the instantiation with texcoords + texel rows
-        lk = count ? dev::render_kernel_lean<true, 6, true, false, true, true>
-                   : dev::render_kernel_lean<false, 6, true, false, true, true>;
-        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, true, true, false>";
-      } else if (mode == KernelMode::kLeanNoPool) {
-        lk = count ? dev::render_kernel_lean<true, 6, true> : dev::render_kernel_lean<false, 6, true>;
-        ctx->last_kernel = "render_kernel_lean<false, 6, true, false, false, false, false>";
-      } else if (mode == KernelMode::kLeanSusp) {
-        lk = count ? dev::render_kernel_lean<true, 6, true, false, false, true, true>
-                   : dev::render_kernel_lean<false, FS_SUSP_WAVES, true, false, false, true, true>;
-        ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_SUSP_WAVES) ", true, false, false, true, true>";
-      } else if (mode == KernelMode::kLeanBvh4) {  // needs a scene uploaded with FS_BVH4=1
-        lk = count ? dev::render_kernel_lean<true, 6, true, true> : dev::render_kernel_lean<false, 6, true, true>;
-        ctx->last_kernel = "render_kernel_lean<false, 6, true, true, false, false, false>";
-      } else if (mode == KernelMode::kLeanIfIf) {
-        lk = count ? dev::render_kernel_lean<true, 6> : dev::render_kernel_lean<false, 6>;
-        ctx->last_kernel = "render_kernel_lean<false, 6, false, false, false, false, false>";
-      }
-      hipLaunchKernelGGL(lk, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
-                         lean.lvl, lean.p0, lean.ovf, lean.tex, lean.rad, (DevCounters*)ctx->counters.p);
-      if (L.groups > 1)
-        hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, lean.rad);
-    } else {
-      hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
-                         (DevCounters*)ctx->counters.p);
-    }
+    hipLaunchKernelGGL(lk, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
+                       rows.lvl, rows.anchor, rows.tex, rows.rad, (DevCounters*)ctx->counters.p);
+    if (L.groups > 1)
+      hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -3263,11 +2162,13 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   return FS_OK;
 }
 
-int fs_prepare_digest(const fs_scene_desc* desc, uint64_t* digest, uint64_t* num_nodes, double* build_ms) {
+int fs_prepare_digest(const fs_scene_desc* desc, const fs_options* opt, uint64_t* digest, uint64_t* num_nodes,
+                      double* build_ms) {
   if (!desc || !digest) return fail(FS_ERR_INVALID, "null argument");
   std::string err;
+  if (opt && !valid_options(opt, &err)) return fail(FS_ERR_INVALID, "fs_prepare_digest: " + err);
   PreparedScene P;
-  int rc = prepare_scene(desc, &P, &err);
+  int rc = prepare_scene(desc, &P, &err, BuildOptions::from(opt));
   if (rc) return fail(rc, err);
   uint64_t h = 1469598103934665603ull;  // FNV-1a over every uploaded array
   auto mix = [&h](const void* p, size_t n) {
@@ -3276,7 +2177,6 @@ int fs_prepare_digest(const fs_scene_desc* desc, uint64_t* digest, uint64_t* num
   };
   mix(P.objects.data(), P.objects.size() * sizeof(DevObject));
   mix(P.nodes.data(), P.nodes.size() * sizeof(BvhNode));
-  mix(P.nodes4.data(), P.nodes4.size() * sizeof(Bvh4Node));
   mix(P.tris.data(), P.tris.size() * sizeof(DevTri));
   mix(P.tri_normals.data(), P.tri_normals.size() * sizeof(float));
   mix(P.tri_tex.data(), P.tri_tex.size() * sizeof(float));
@@ -3345,42 +2245,117 @@ int fs_comm_destroy(fs_context* ctx) {
   return FS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The tile exchange of a multi-GPU frame: pack_tiles writes a rank's owned
+// tiles (tile t of rank r is t = r + k * nranks) as kPackWords words per
+// pixel; unpack_tiles scatters nranks such packs, concatenated in rank order
+// as ncclGather delivers them, into the root's frame (skipping its own).
+struct TileExchange {
+  Launch L{};
+  uint32_t owned_max = 0;
+  size_t pixels = 0;  // per rank
+  size_t bytes() const { return pixels * dev::kPackWords * 4; }
+};
+int tile_exchange(const fs_render_params* params, fs_frame* frame, uint32_t nranks, uint32_t rank, TileExchange* X) {
+  uint32_t ts, stride;
+  int rc = check_params(params, frame, &ts, &stride);
+  if (rc) return rc;
+  if (stride != nranks || params->tile_offset != rank)
+    return fail(FS_ERR_INVALID, "tiling must be tile_offset=rank, tile_stride=nranks");
+  X->L.tile_size = ts;
+  X->L.tiles_x = (params->width + ts - 1) / ts;
+  X->L.tile_offset = params->tile_offset;
+  X->L.tile_stride = stride;
+  const uint32_t tiles = X->L.tiles_x * ((params->height + ts - 1) / ts);
+  X->owned_max = (tiles + stride - 1) / stride;
+  X->pixels = (size_t)X->owned_max * ts * ts;
+  return FS_OK;
+}
+int launch_pack(fs_context* ctx, fs_frame* frame, const TileExchange& X, uint32_t* dst) {
+  hipLaunchKernelGGL(dev::pack_tiles, dim3((uint32_t)((X.pixels + 255) / 256)), dim3(256), 0, ctx->stream,
+                     frame_view(frame), X.L, X.owned_max, dst);
+  FS_HIP(hipGetLastError());
+  return FS_OK;
+}
+int launch_unpack(fs_context* ctx, fs_frame* frame, const TileExchange& X, uint32_t nranks, uint32_t self,
+                  const uint32_t* src) {
+  const size_t total = X.pixels * nranks;
+  hipLaunchKernelGGL(dev::unpack_tiles, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, ctx->stream,
+                     frame_view(frame), X.L, X.owned_max, nranks, self, src);
+  FS_HIP(hipGetLastError());
+  return FS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 // Packs this rank's owned tiles, ncclGather's them to root over xGMI and
 // scatters them into root's frame. One collective per render.
 int fs_frame_gather(fs_context* ctx, fs_frame* frame, const fs_render_params* params, int root) {
   if (!ctx || !frame || !params) return fail(FS_ERR_INVALID, "null argument");
   if (!ctx->comm) return fail(FS_ERR_STATE, "fs_frame_gather before fs_comm_init");
-  uint32_t ts, stride;
-  int rc = check_params(params, frame, &ts, &stride);
+  TileExchange X;
+  int rc = tile_exchange(params, frame, (uint32_t)ctx->nranks, (uint32_t)ctx->rank, &X);
   if (rc) return rc;
-  if ((int)stride != ctx->nranks || (int)params->tile_offset != ctx->rank)
-    return fail(FS_ERR_INVALID, "tiling must be tile_offset=rank, tile_stride=nranks");
   if (root < 0 || root >= ctx->nranks) return fail(FS_ERR_INVALID, "root out of range");
   if ((rc = set_device(ctx))) return rc;
-  Launch L{};
-  L.tile_size = ts;
-  L.tiles_x = (params->width + ts - 1) / ts;
-  L.tile_offset = params->tile_offset;
-  L.tile_stride = stride;
-  uint32_t tiles = L.tiles_x * ((params->height + ts - 1) / ts);
-  uint32_t owned_max = (tiles + stride - 1) / stride;
-  size_t per_rank_words = (size_t)owned_max * ts * ts * dev::kPackWords;
-  if ((rc = ensure(&ctx->pack_send, per_rank_words * 4))) return rc;
-  if (ctx->rank == root && (rc = ensure(&ctx->pack_recv, per_rank_words * 4 * ctx->nranks))) return rc;
-  DevFrame F = frame_view(frame);
-  size_t n = (size_t)owned_max * ts * ts;
-  hipLaunchKernelGGL(dev::pack_tiles, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, ctx->stream, F, L, owned_max,
-                     (uint32_t*)ctx->pack_send.p);
-  FS_HIP(hipGetLastError());
-  ncclResult_t r = ncclGather(ctx->pack_send.p, ctx->rank == root ? ctx->pack_recv.p : nullptr, per_rank_words,
+  if ((rc = ensure(&ctx->pack_send, X.bytes()))) return rc;
+  if (ctx->rank == root && (rc = ensure(&ctx->pack_recv, X.bytes() * ctx->nranks))) return rc;
+  if ((rc = launch_pack(ctx, frame, X, (uint32_t*)ctx->pack_send.p))) return rc;
+  ncclResult_t r = ncclGather(ctx->pack_send.p, ctx->rank == root ? ctx->pack_recv.p : nullptr, X.bytes() / 4,
                               ncclUint32, root, ctx->comm, ctx->stream);
   if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
-  if (ctx->rank == root) {
-    size_t total = n * ctx->nranks;
-    hipLaunchKernelGGL(dev::unpack_tiles, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, ctx->stream, F, L,
-                       owned_max, (uint32_t)ctx->nranks, (uint32_t)ctx->rank, (const uint32_t*)ctx->pack_recv.p);
-    FS_HIP(hipGetLastError());
-  }
+  if (ctx->rank == root &&
+      (rc = launch_unpack(ctx, frame, X, (uint32_t)ctx->nranks, (uint32_t)ctx->rank, (const uint32_t*)ctx->pack_recv.p)))
+    return rc;
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  return FS_OK;
+}
+
+int fs_frame_pack_bytes(const fs_render_params* params, uint64_t* bytes) {
+  if (!params || !bytes) return fail(FS_ERR_INVALID, "null argument");
+  fs_frame probe;
+  probe.width = params->width;
+  probe.height = params->height;
+  TileExchange X;
+  int rc = tile_exchange(params, &probe, params->tile_stride ? params->tile_stride : 1, params->tile_offset, &X);
+  if (rc) return rc;
+  *bytes = X.bytes();
+  return FS_OK;
+}
+
+int fs_frame_pack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, void* host_dst, size_t bytes) {
+  if (!ctx || !frame || !params || !host_dst) return fail(FS_ERR_INVALID, "null argument");
+  if (frame->ctx != ctx) return fail(FS_ERR_INVALID, "frame belongs to another context");
+  TileExchange X;
+  int rc = tile_exchange(params, frame, params->tile_stride ? params->tile_stride : 1, params->tile_offset, &X);
+  if (rc) return rc;
+  if (bytes != X.bytes()) return fail(FS_ERR_INVALID, "byte count does not match fs_frame_pack_bytes");
+  if ((rc = set_device(ctx))) return rc;
+  if ((rc = ensure(&ctx->pack_send, X.bytes()))) return rc;
+  if ((rc = launch_pack(ctx, frame, X, (uint32_t*)ctx->pack_send.p))) return rc;
+  FS_HIP(hipMemcpyAsync(host_dst, ctx->pack_send.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  FS_HIP(hipStreamSynchronize(ctx->stream));
+  return FS_OK;
+}
+
+int fs_frame_unpack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, const void* host_src,
+                    size_t bytes) {
+  if (!ctx || !frame || !params || !host_src) return fail(FS_ERR_INVALID, "null argument");
+  if (frame->ctx != ctx) return fail(FS_ERR_INVALID, "frame belongs to another context");
+  const uint32_t nranks = params->tile_stride ? params->tile_stride : 1;
+  TileExchange X;
+  int rc = tile_exchange(params, frame, nranks, params->tile_offset, &X);
+  if (rc) return rc;
+  if (bytes != X.bytes() * nranks) return fail(FS_ERR_INVALID, "byte count must be nranks x fs_frame_pack_bytes");
+  if ((rc = set_device(ctx))) return rc;
+  if ((rc = ensure(&ctx->pack_recv, bytes))) return rc;
+  FS_HIP(hipMemcpyAsync(ctx->pack_recv.p, host_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = launch_unpack(ctx, frame, X, nranks, params->tile_offset, (const uint32_t*)ctx->pack_recv.p))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
   return FS_OK;
 }

@@ -5,8 +5,9 @@
 // (primitive tests), material.cpp + normal.cpp (BRDF sampling and shading)
 // and frame.cpp:53-85 (running-mean accumulation). The recursion of TraceStep
 // is unrolled into a forward pass that stages each bounce's shading scalars
-// in LDS and a backward pass that applies Material::Sample in the reference's
-// order, so the float rounding matches the recursive reference bit for bit.
+// in per-lane HBM scratch rows (L2-resident) and a backward
+// pass that applies Material::Sample in the reference's order, so the float
+// rounding matches the recursive reference bit for bit.
 #pragma once
 
 #include "fs_scene.h"
@@ -27,7 +28,6 @@ constexpr uint64_t kGroupTargetBlocks = 262144;
 struct DevScene {
   const DevObject* __restrict__ objects;
   const BvhNode* __restrict__ nodes;
-  const Bvh4Node* __restrict__ nodes4;
   const DevTri* __restrict__ tris;
   const float4* __restrict__ tri_normals;
   const fs_material* __restrict__ materials;

@@ -169,25 +169,10 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
 }
 
 constexpr int kMaxBins = 64;
-// SAH bins per axis (FS_BVH_BINS overrides, for tuning).
-int bins_env() {
-  int v = std::getenv("FS_BVH_BINS") ? std::atoi(std::getenv("FS_BVH_BINS")) : 16;
-  return (v >= 2 && v <= kMaxBins) ? v : 16;
-}
-// Target leaf size (FS_BVH_LEAF overrides, for tuning).
-uint32_t leaf_target_env() {
-  uint32_t v = std::getenv("FS_BVH_LEAF") ? (uint32_t)std::atoi(std::getenv("FS_BVH_LEAF")) : 2u;
-  return (v && v <= kMaxLeafCount) ? v : 2u;
-}
-
-// FS_NODE_LAYOUT=pairs: sibling inner nodes share one 128-B line (an
-// even/odd slot pair), so the far child of a visited node arrives with the
-// near one. Node order never changes a hit (closest hit is a total order).
-bool pair_layout_env() {
-  const char* e = std::getenv("FS_NODE_LAYOUT");
-  return e && std::strcmp(e, "pairs") == 0;
-}
-
+// fs_options.node_layout = FS_NODE_LAYOUT_PAIRS: sibling inner nodes share
+// one 128-B line (an even/odd slot pair), so the far child of a visited node
+// arrives with the near one. Node order never changes a hit (closest hit is
+// a total order).
 // Rewrites the nodes [begin, end) of one mesh (root at begin, begin even) in
 // the pair layout: root, then per node (depth first) its inner children as
 // one aligned pair, padding with an unused slot where a pair would straddle.
@@ -224,27 +209,29 @@ void relayout_pairs(std::vector<BvhNode>* nodes, uint32_t begin) {
 }
 
 // Subtrees are built concurrently down to this depth (2^depth threads);
-// FS_BVH_THREADS=1 builds sequentially (same tree, same layout).
-uint32_t parallel_depth_env() {
-  const char* e = std::getenv("FS_BVH_THREADS");
-  if (!e) return 4;
-  int t = std::atoi(e), d = 0;
-  while (d < 8 && (1 << (d + 1)) <= t) d++;
-  return (uint32_t)d;
+// fs_options.bvh_threads = 1 builds sequentially (same tree, same layout).
+uint32_t parallel_depth(uint32_t threads) {
+  if (!threads) return 4;
+  uint32_t d = 0;
+  while (d < 8 && (1u << (d + 1)) <= threads) d++;
+  return d;
 }
 
 class BvhBuilder {
  public:
   BvhBuilder(std::vector<BvhNode>* nodes, std::vector<DevTri>* tris, std::vector<float>* tri_normals,
              std::vector<float>* tri_tex, const std::vector<DevTri>* mesh_tris,
-             const std::vector<float>* mesh_normals, const std::vector<float>* mesh_tex)
+             const std::vector<float>* mesh_normals, const std::vector<float>* mesh_tex, const BuildOptions& opt)
       : nodes_(nodes),
         tris_(tris),
         tri_normals_(tri_normals),
         tri_tex_(tri_tex),
         mesh_tris_(mesh_tris),
         mesh_normals_(mesh_normals),
-        mesh_tex_(mesh_tex) {}
+        mesh_tex_(mesh_tex),
+        leaf_(opt.leaf),
+        bins_(opt.bins),
+        par_depth_(parallel_depth(opt.threads)) {}
 
   // Builds the tree over all faces; returns the root node index.
   uint32_t build(std::vector<Prim>& prims, uint32_t* max_depth) {
@@ -396,7 +383,8 @@ class BvhBuilder {
     std::unique_ptr<BvhBuilder> b;
   };
   void init_local(Local* L) const {
-    L->b.reset(new BvhBuilder(&L->nodes, &L->tris, &L->normals, &L->tex, mesh_tris_, mesh_normals_, mesh_tex_));
+    L->b.reset(new BvhBuilder(&L->nodes, &L->tris, &L->normals, &L->tex, mesh_tris_, mesh_normals_, mesh_tex_,
+                              BuildOptions{}));
     L->b->prims_ = prims_;
     L->b->leaf_ = leaf_;
     L->b->bins_ = bins_;
@@ -471,104 +459,12 @@ class BvhBuilder {
   const std::vector<float>* mesh_normals_;
   const std::vector<float>* mesh_tex_;
   std::vector<Prim>* prims_ = nullptr;
-  uint32_t leaf_ = leaf_target_env();
-  int bins_ = bins_env();
-  uint32_t par_depth_ = parallel_depth_env();
+  uint32_t leaf_;
+  int bins_;
+  uint32_t par_depth_;
   uint32_t max_depth_ = 0;
   bool overflow_ = false;
 };
-
-// Collapses a BVH2 into a BVH4: a node's four slots are filled by repeatedly
-// opening the inner child with the largest box surface. Leaves and their
-// triangle ranges are shared with the BVH2. Returns the BVH4 root, or -1 when
-// the worst-case traversal stack (sum over a root-to-leaf path of the pushes
-// per node) would not fit kTraversalStack + kStackOverflow.
-class Collapse4 {
- public:
-  Collapse4(const std::vector<BvhNode>& n2, std::vector<Bvh4Node>* n4) : n2_(n2), n4_(n4) {}
-  int32_t run(uint32_t root2) {
-    size_t mark = n4_->size();
-    uint32_t need = 0;
-    uint32_t r = node(root2, &need);
-    if (need + 1 > kTraversalStack + kStackOverflow) {
-      n4_->resize(mark);
-      return -1;
-    }
-    return (int32_t)r;
-  }
-
- private:
-  struct Slot {
-    float lo[3], hi[3];
-    uint32_t word;
-    float area() const {
-      float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-      return dx * dy + dy * dz + dz * dx;
-    }
-  };
-  static bool empty_slot(const BvhNode& n, int s) { return (n.child[s] & kLeafBit) && n.lo_x[s] >= 1e30f; }
-  static Slot slot_of(const BvhNode& n, int s) {
-    Slot o;
-    o.lo[0] = n.lo_x[s];
-    o.lo[1] = n.lo_y[s];
-    o.lo[2] = n.lo_z[s];
-    o.hi[0] = n.hi_x[s];
-    o.hi[1] = n.hi_y[s];
-    o.hi[2] = n.hi_z[s];
-    o.word = n.child[s];
-    return o;
-  }
-  uint32_t node(uint32_t i2, uint32_t* need) {
-    std::vector<Slot> slots;
-    for (int s = 0; s < 2; s++)
-      if (!empty_slot(n2_[i2], s)) slots.push_back(slot_of(n2_[i2], s));
-    while (slots.size() < 4) {
-      int best = -1;
-      for (size_t k = 0; k < slots.size(); k++)
-        if (!(slots[k].word & kLeafBit) && (best < 0 || slots[k].area() > slots[best].area())) best = (int)k;
-      if (best < 0) break;
-      const BvhNode& c = n2_[slots[best].word];
-      slots.erase(slots.begin() + best);
-      for (int s = 0; s < 2; s++)
-        if (!empty_slot(c, s)) slots.push_back(slot_of(c, s));
-    }
-    uint32_t me = (uint32_t)n4_->size();
-    n4_->emplace_back();
-    uint32_t sub = 0;
-    for (size_t k = 0; k < slots.size(); k++) {
-      if (!(slots[k].word & kLeafBit)) {
-        uint32_t cn = 0;
-        slots[k].word = node(slots[k].word, &cn);
-        sub = std::max(sub, cn);
-      }
-    }
-    Bvh4Node& o = (*n4_)[me];
-    std::memset(&o, 0, sizeof(o));
-    for (int k = 0; k < 4; k++) {
-      if (k < (int)slots.size()) {
-        const Slot& sl = slots[k];
-        o.lo_x[k] = sl.lo[0], o.lo_y[k] = sl.lo[1], o.lo_z[k] = sl.lo[2];
-        o.hi_x[k] = sl.hi[0], o.hi_y[k] = sl.hi[1], o.hi_z[k] = sl.hi[2];
-        o.child[k] = sl.word;
-      } else {
-        o.lo_x[k] = o.lo_y[k] = o.lo_z[k] = o.hi_x[k] = o.hi_y[k] = o.hi_z[k] = 3e30f;
-        o.child[k] = kLeafBit;  // empty leaf
-      }
-    }
-    uint32_t pushes = slots.empty() ? 0 : (uint32_t)slots.size() - 1;
-    *need = pushes + sub;
-    return me;
-  }
-  const std::vector<BvhNode>& n2_;
-  std::vector<Bvh4Node>* n4_;
-};
-
-// BVH4 collapse is opt-in (FS_BVH4=1, FS_KERNEL=lean_bvh4): measured slower
-// than the BVH2 on MI355X.
-bool bvh4_enabled() {
-  const char* e = std::getenv("FS_BVH4");
-  return e && std::atoi(e) != 0;
-}
 
 void cube_planes(const f3* v, float* d) {  // volume.cpp:234-247
   f4 p[6] = {plane_3p(v[0], v[1], v[2]), plane_3p(v[6], v[5], v[4]), plane_3p(v[5], v[6], v[2]),
@@ -703,9 +599,22 @@ void parallel_chunks(uint32_t n, F&& fn) {
   for (std::thread& th : pool) th.join();
 }
 
-uint32_t bvh_leaf_target() { return leaf_target_env(); }
+BuildOptions BuildOptions::from(const fs_options* o) {
+  fs_options def;
+  fs_options_default(&def);
+  if (!o) o = &def;
+  BuildOptions b;
+  b.leaf = (o->bvh_leaf && o->bvh_leaf <= kMaxLeafCount) ? o->bvh_leaf : def.bvh_leaf;
+  b.bins = (o->bvh_bins >= 2 && o->bvh_bins <= (uint32_t)kMaxBins) ? (int)o->bvh_bins : (int)def.bvh_bins;
+  b.threads = o->bvh_threads;
+  b.pair_layout = o->node_layout == FS_NODE_LAYOUT_PAIRS;
+  b.park_min_tris = o->park_min_tris;
+  b.log = o->build_log != 0;
+  return b;
+}
 
-int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, uint32_t gpu_bvh_min_tris) {
+int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, const BuildOptions& opt,
+                  uint32_t gpu_bvh_min_tris) {
   auto t0 = std::chrono::steady_clock::now();
   if (!d || !out) {
     *err = "null scene";
@@ -771,14 +680,12 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   // Meshes: MeshObject::MeshObject + BuildBvh face planes.
   struct MeshOut {
     uint32_t root = 0;
-    int32_t root4 = -1;
     bool tree = false;
     bool normals = false;
     bool texcoords = false;
     Bounds rb;
   };
   std::vector<MeshOut> mesh_out(d->num_meshes);
-  const bool use4 = bvh4_enabled();
   bool any_normals = false, any_tex = false;
   size_t all_tris = 0;
   for (uint32_t mi = 0; mi < d->num_meshes; mi++) {
@@ -925,7 +832,6 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.tris = std::move(mtris);
       if (any_normals) D.normals = std::move(mnormals);
       if (any_tex) D.tex = std::move(mtex);
-      mesh_out[mi].root4 = -1;
       S.deferred.push_back(std::move(D));
       continue;
     }
@@ -939,18 +845,18 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       for (int k = 0; k < 3; k++) p.c[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
       p.face = f;
     }
-    const bool pairs = !use4 && pair_layout_env();
+    const bool pairs = opt.pair_layout;
     if (pairs && (S.nodes.size() & 1u)) {
       BvhNode blank;
       std::memset(&blank, 0, sizeof(blank));
       S.nodes.push_back(blank);
     }
     const uint32_t node_begin = (uint32_t)S.nodes.size();
-    BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex);
+    BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex, opt);
     auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
     if (pairs && mesh_out[mi].root == node_begin) relayout_pairs(&S.nodes, node_begin);
-    if (std::getenv("FS_BUILD_LOG"))
+    if (opt.log)
       std::fprintf(stderr, "[fs build] mesh %u: %u tris, prepare %.1f ms, prims %.1f ms, bvh %.1f ms\n", mi,
                    m.num_triangles, std::chrono::duration<double, std::milli>(tp - t0).count(),
                    std::chrono::duration<double, std::milli>(tb - tp).count(),
@@ -959,7 +865,6 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
       return FS_ERR_INVALID;
     }
-    mesh_out[mi].root4 = use4 ? Collapse4(S.nodes, &S.nodes4).run(mesh_out[mi].root) : -1;
   }
 
   // Device-built meshes take the node and triangle slots after the host arrays.
@@ -976,10 +881,9 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     }
   }
 
-  // FS_PARK_MIN_TRIS lowers the parking threshold (tests exercise the SUSP
-  // schedule on small meshes with it).
-  const char* pe = std::getenv("FS_PARK_MIN_TRIS");
-  const uint32_t park_min = pe ? (uint32_t)std::strtoul(pe, nullptr, 10) : kParkMinTris;
+  // fs_options.park_min_tris (tests exercise the parked-walk schedule on
+  // small meshes by lowering it).
+  const uint32_t park_min = opt.park_min_tris;
   S.objects.resize(d->num_objects);
   for (uint32_t i = 0; i < d->num_objects; i++) {
     const fs_object& o = d->objects[i];
@@ -1000,7 +904,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i0 = (int32_t)mo.root;
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
-      D.i3 = mo.tree ? mo.root4 : -1;
+      D.i3 = 0;
       D.i4 = mo.texcoords ? 1 : 0;
       D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);

@@ -26,7 +26,7 @@ struct DevObject {
   int32_t i0;    // MESH: BVH root node index
   int32_t i1;    // MESH: 1 if the mesh has vertex normals
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
-  int32_t i3;    // MESH: BVH4 root node index, or -1 (traverse the BVH2)
+  int32_t i3;    // unused (0)
   int32_t i4;    // MESH: 1 if the mesh has texcoords (mesh.cpp:300)
   int32_t i5;    // MESH: 1 if its walks may park (>= kParkMinTris triangles, SUSP schedule)
   float d[40];
@@ -52,25 +52,10 @@ struct BvhNode {
   uint32_t pad[2];
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
-// BVH4 node, 128 B: four child boxes (SoA over the children) + 4 child
-// words, collapsed from the BVH2 (fs_scene.cpp collapse4). Same child-word
-// encoding; an unused slot is an empty leaf (count 0) with a far point box.
-struct Bvh4Node {
-  float lo_x[4], hi_x[4];
-  float lo_y[4], hi_y[4];
-  float lo_z[4], hi_z[4];
-  uint32_t child[4];
-  uint32_t pad[4];
-};
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kMaxLeafCount = 127;
 constexpr uint32_t kMaxTriangles = 1u << 24;
 constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
-// BVH4 traversal keeps kTraversalStack entries in LDS and spills deeper ones
-// to a per-lane HBM row of kStackOverflow entries; a mesh whose worst-case
-// stack need exceeds the sum keeps the BVH2 (collapse4 checks).
-constexpr uint32_t kStackOverflow = 40;
 
 // Triangle record: the operands of the reference test (intersect.cpp:357-419)
 // with every ray-independent term precomputed on the host by the same float
@@ -131,7 +116,6 @@ struct DeferredMesh {
 struct PreparedScene {
   std::vector<DevObject> objects;
   std::vector<BvhNode> nodes;
-  std::vector<Bvh4Node> nodes4;
   std::vector<DevTri> tris;
   std::vector<float> tri_normals;  // 12 floats per triangle (n0,n1,n2 + pad) or empty
   std::vector<float> tri_tex;      // 6 floats per triangle (t0,t1,t2) or empty
@@ -147,13 +131,23 @@ struct PreparedScene {
   bool any_normals = false, any_tex = false;       // per-triangle normal / texcoord arrays exist
 };
 
+// The scene-build part of fs_options, validated (out-of-range values take
+// the defaults).
+struct BuildOptions {
+  uint32_t leaf = 2;            // faces per BVH leaf (both builders)
+  int bins = 16;                // SAH bins per axis
+  uint32_t threads = 0;         // host build threads, 0 = 16
+  bool pair_layout = false;     // sibling-pair node layout (host build)
+  uint32_t park_min_tris = kParkMinTris;
+  bool log = false;             // build phases to stderr
+  static BuildOptions from(const fs_options* o);  // NULL: the defaults
+};
+
 // Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
 // one SAH BVH per mesh. Returns FS_OK or an fs_status with *err set.
 // Meshes of at least gpu_bvh_min_tris triangles (0: none) are not built
 // here but deferred to the device build (PreparedScene::deferred).
-int prepare_scene(const fs_scene_desc* desc, PreparedScene* out, std::string* err, uint32_t gpu_bvh_min_tris = 0);
-
-// The leaf-size target both builders use (FS_BVH_LEAF overrides, default 2).
-uint32_t bvh_leaf_target();
+int prepare_scene(const fs_scene_desc* desc, PreparedScene* out, std::string* err, const BuildOptions& opt,
+                  uint32_t gpu_bvh_min_tris = 0);
 
 }  // namespace fs

@@ -87,7 +87,17 @@ class fs_counters(C.Structure):
                 ("tri_tests", C.c_uint64), ("prim_tests", C.c_uint64)]
 
 
+class fs_options(C.Structure):
+    _fields_ = [("schedule", C.c_int32), ("park_lanes", C.c_uint32), ("park_min_tris", C.c_uint32),
+                ("samples_per_block", C.c_uint32), ("groups", C.c_uint32), ("group_major", C.c_uint32),
+                ("tile_order", C.c_uint32), ("xcd_bands", C.c_uint32), ("gpu_bvh_min_tris", C.c_uint32),
+                ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
+                ("node_layout", C.c_uint32), ("build_log", C.c_uint32)]
+
+
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
+SCHEDULES = {"auto": 0, "lean": 1, "parked": 2}  # fs_schedule
+NODE_LAYOUTS = {"depth_first": 0, "pairs": 1}
 
 # Exported symbols of include/fs_trace.h, with their ctypes signatures.
 _VP = C.c_void_p
@@ -97,6 +107,9 @@ GPU_SYMBOLS = {
     "fs_device_count": ([C.POINTER(C.c_int)], C.c_int),
     "fs_create": ([C.c_int, C.POINTER(_VP)], C.c_int),
     "fs_destroy": ([_VP], C.c_int),
+    "fs_options_default": ([C.POINTER(fs_options)], C.c_int),
+    "fs_set_options": ([_VP, C.POINTER(fs_options)], C.c_int),
+    "fs_get_options": ([_VP, C.POINTER(fs_options)], C.c_int),
     "fs_upload_scene": ([_VP, _VP], C.c_int),
     "fs_upload_scene_ex": ([_VP, _VP, C.c_uint32], C.c_int),
     "fs_scene_stats": ([_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
@@ -116,7 +129,11 @@ GPU_SYMBOLS = {
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
     "fs_comm_destroy": ([_VP], C.c_int),
-    "fs_prepare_digest": ([_VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double)], C.c_int),
+    "fs_frame_pack_bytes": ([C.POINTER(fs_render_params), C.POINTER(C.c_uint64)], C.c_int),
+    "fs_frame_pack": ([_VP, _VP, C.POINTER(fs_render_params), _VP, C.c_size_t], C.c_int),
+    "fs_frame_unpack": ([_VP, _VP, C.POINTER(fs_render_params), _VP, C.c_size_t], C.c_int),
+    "fs_prepare_digest": ([_VP, C.POINTER(fs_options), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                           C.POINTER(C.c_double)], C.c_int),
     "fs_trace_range": ([_VP, C.POINTER(fs_camera), C.c_uint32, C.c_uint32, _VP, C.c_uint32, _VP], C.c_int),
 }
 HOST_SYMBOLS = {
@@ -335,26 +352,71 @@ class Frame:
             self.h = None
 
 
+def options(**kw):
+    """fs_options: the defaults (fs_options_default) with fields replaced by
+    keyword; schedule and node_layout also take their names."""
+    o = fs_options()
+    _check(gpu_lib().fs_options_default(C.byref(o)), "fs_options_default")
+    names = {k for k, _ in fs_options._fields_}
+    for k, v in kw.items():
+        if k not in names:
+            raise FsError(f"unknown fs_options field {k!r}")
+        if k == "schedule" and isinstance(v, str):
+            v = SCHEDULES[v]
+        if k == "node_layout" and isinstance(v, str):
+            v = NODE_LAYOUTS[v]
+        setattr(o, k, int(v))
+    return o
+
+
+def options_dict(o):
+    return {k: getattr(o, k) for k, _ in fs_options._fields_}
+
+
+def parse_variant(v):
+    """'schedule=lean@park_lanes=8' -> {'schedule': 'lean', 'park_lanes': 8}
+    (tools' A/B variant syntax; 'default' -> {})."""
+    out = {}
+    for kv in v.split("@"):
+        if not kv or kv == "default":
+            continue
+        k, val = kv.split("=", 1)
+        out[k] = val if k in ("schedule", "node_layout") else int(val)
+    return out
+
+
 class Renderer:
     """One fs_context (one GPU, one stream)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, **opts):
         lib = gpu_lib()
         h = C.c_void_p()
         _check(lib.fs_create(device, C.byref(h)), "fs_create")
         self.ctx = h
         self._scene_ref = None
+        if opts:
+            self.set_options(**opts)
 
-    def upload(self, scene, gpu_bvh=None):
+    def set_options(self, **kw):
+        """fs_set_options with the given fields changed from the current ones."""
+        o = self.get_options()
+        for k, v in options_dict(options(**kw)).items():
+            if k in kw:
+                setattr(o, k, v)
+        _check(gpu_lib().fs_set_options(self.ctx, C.byref(o)), "fs_set_options")
+
+    def get_options(self):
+        o = fs_options()
+        _check(gpu_lib().fs_get_options(self.ctx, C.byref(o)), "fs_get_options")
+        return o
+
+    def upload(self, scene, gpu_bvh=False):
         """scene: HostScene, or a ctypes pointer/void* to an fs_scene_desc.
-        gpu_bvh: True/False selects the device/host BVH build of large meshes
-        (fs_upload_scene_ex); None keeps fs_upload_scene (FS_GPU_BVH env)."""
+        gpu_bvh: build the BVH of large meshes on the device
+        (fs_upload_scene_ex FS_UPLOAD_GPU_BVH) or on the host."""
         ptr = scene.desc_ptr() if isinstance(scene, HostScene) else scene
-        if gpu_bvh is None:
-            _check(gpu_lib().fs_upload_scene(self.ctx, ptr), "fs_upload_scene")
-        else:
-            flags = UPLOAD_GPU_BVH if gpu_bvh else 0
-            _check(gpu_lib().fs_upload_scene_ex(self.ctx, ptr, flags), "fs_upload_scene_ex")
+        flags = UPLOAD_GPU_BVH if gpu_bvh else 0
+        _check(gpu_lib().fs_upload_scene_ex(self.ctx, ptr, flags), "fs_upload_scene_ex")
         self._scene_ref = scene
 
     def scene_stats(self):
@@ -421,6 +483,21 @@ class Renderer:
     def gather(self, frame, params, root=0):
         _check(gpu_lib().fs_frame_gather(self.ctx, frame.h, C.byref(params), root), "fs_frame_gather")
 
+    def pack(self, frame, params):
+        """fs_frame_pack: this rank's owned tiles as uint32 words (40 B per pixel)."""
+        n = C.c_uint64()
+        _check(gpu_lib().fs_frame_pack_bytes(C.byref(params), C.byref(n)), "fs_frame_pack_bytes")
+        out = np.zeros(n.value // 4, np.uint32)
+        _check(gpu_lib().fs_frame_pack(self.ctx, frame.h, C.byref(params), out.ctypes.data, out.nbytes),
+               "fs_frame_pack")
+        return out
+
+    def unpack(self, frame, params, packs):
+        """fs_frame_unpack: scatters the rank-ordered concatenation of packs."""
+        buf = np.ascontiguousarray(np.concatenate(packs), np.uint32)
+        _check(gpu_lib().fs_frame_unpack(self.ctx, frame.h, C.byref(params), buf.ctypes.data, buf.nbytes),
+               "fs_frame_unpack")
+
     def close(self):
         if self.ctx:
             gpu_lib().fs_destroy(self.ctx)
@@ -455,8 +532,11 @@ def load_exr(path):
         lib.fsh_free(buf)
 
 
-def prepare_digest(desc_ptr):
-    """fs_prepare_digest: host-only scene preparation; (digest, nodes, build_ms)."""
+def prepare_digest(desc_ptr, **opts):
+    """fs_prepare_digest: host-only scene preparation with the build fields
+    of fs_options (keywords as options()); (digest, nodes, build_ms)."""
     d, n, ms = C.c_uint64(), C.c_uint64(), C.c_double()
-    _check(gpu_lib().fs_prepare_digest(desc_ptr, C.byref(d), C.byref(n), C.byref(ms)), "fs_prepare_digest")
+    o = options(**opts)
+    _check(gpu_lib().fs_prepare_digest(desc_ptr, C.byref(o), C.byref(d), C.byref(n), C.byref(ms)),
+           "fs_prepare_digest")
     return d.value, n.value, ms.value

@@ -925,6 +925,8 @@ struct Engine {
   int status = FS_OK;
   std::string error;
   uint32 frame_counter = 0;
+  TraceSettings settings;
+  bool settings_init = false;
 };
 Engine& engine() {
   static Engine e;
@@ -936,10 +938,18 @@ int engine_fail(Engine& e, int rc, const std::string& where) {
   std::fprintf(stderr, "[fs] %s\n", e.error.c_str());
   return rc;
 }
+void init_settings(Engine& e) {
+  if (e.settings_init) return;
+  fs_options_default(&e.settings.options);
+  e.settings_init = true;
+}
 int ensure_context(Engine& e) {
   if (e.ctx) return FS_OK;
+  init_settings(e);
   int rc = fs_create(e.device, &e.ctx);
   if (rc) return engine_fail(e, rc, "fs_create");
+  rc = fs_set_options(e.ctx, &e.settings.options);
+  if (rc) return engine_fail(e, rc, "fs_set_options");
   return FS_OK;
 }
 }  // namespace
@@ -949,6 +959,29 @@ bool SetTraceDevice(int device) {
   std::lock_guard<std::mutex> g(e.mu);
   if (e.ctx) return false;
   e.device = device;
+  return true;
+}
+TraceSettings GetTraceSettings() {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  init_settings(e);
+  return e.settings;
+}
+bool SetTraceSettings(const TraceSettings& s) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  init_settings(e);
+  if (e.ctx) {
+    int rc = fs_set_options(e.ctx, &s.options);
+    if (rc) {
+      engine_fail(e, rc, "fs_set_options");
+      return false;
+    }
+  }
+  const bool rebuild = std::memcmp(&s.options, &e.settings.options, sizeof(fs_options)) != 0 ||
+                       s.device_bvh != e.settings.device_bvh;
+  e.settings = s;
+  if (rebuild) e.scene = nullptr;  // re-upload with the new build settings
   return true;
 }
 int LastTraceStatus() { return engine().status; }
@@ -1003,9 +1036,8 @@ bool ensure_scene(Engine& e, Scene* scene) {
       return false;
     }
     // Large meshes get their BVH built on the device (same frames, about a
-    // tenth of the host build time); FS_GPU_BVH=0 keeps the host build.
-    const char* gb = std::getenv("FS_GPU_BVH");
-    const uint32_t flags = (gb && std::strcmp(gb, "0") == 0) ? 0u : FS_UPLOAD_GPU_BVH;
+    // tenth of the host build time) unless TraceSettings::device_bvh is off.
+    const uint32_t flags = e.settings.device_bvh ? FS_UPLOAD_GPU_BVH : 0u;
     int rc = fs_upload_scene_ex(e.ctx, d, flags);
     if (rc) {
       engine_fail(e, rc, "fs_upload_scene_ex");
@@ -1035,18 +1067,34 @@ void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uin
   std::memset(&p, 0, sizeof(p));
   p.width = output->GetWidth();
   p.height = output->GetHeight();
-  p.spp = spp;
-  p.sample_base = output->samples();
   auto t0 = std::chrono::steady_clock::now();
-  int rc = fs_render(e.ctx, &cam, &p, output->device_frame());
-  if (!rc) rc = fs_synchronize(e.ctx);
+  // The C ABI seeds sample k of a pixel from (pixel << 20) ^ k ^ seed with
+  // k < 2^20; a frame that keeps accumulating past 2^20 samples (the
+  // reference has no limit) moves on to epoch e = samples >> 20 with seed
+  // e << 48, above every pixel bit of frames up to 2^28 pixels.
+  uint64 have = output->samples();
+  for (uint32 left = spp; left;) {
+    const uint64 epoch = have >> 20, k = have & ((1u << 20) - 1);
+    const uint32 n = (uint32)std::min<uint64>(left, (1u << 20) - k);
+    p.spp = n;
+    p.sample_base = (uint32)k;
+    p.seed = epoch << 48;
+    int rc = fs_render(e.ctx, &cam, &p, output->device_frame());
+    if (rc) {
+      engine_fail(e, rc, "fs_render");
+      return;
+    }
+    have += n;
+    left -= n;
+  }
+  int rc = fs_synchronize(e.ctx);
   if (rc) {
-    engine_fail(e, rc, "fs_render");
+    engine_fail(e, rc, "fs_synchronize");
     return;
   }
   output->add_samples(spp);
   double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (!view.fast_render_enabled && std::getenv("FS_TRACE_LOG"))  // engine.cpp:284-293
+  if (!view.fast_render_enabled && e.settings.timing_log)  // engine.cpp:284-293
     std::printf("Frame %u render time: %.2f sec. Msamples/sec: %.2f\n", e.frame_counter, sec,
                 (double)p.width * p.height * spp / (1e6 * sec));
   e.frame_counter++;

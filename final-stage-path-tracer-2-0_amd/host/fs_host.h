@@ -356,11 +356,12 @@ class DisplayFrame {
   void SetFrameCount(uint32 count) { frame_count_ = count; }
   uint32 GetFrameCount() const { return frame_count_; }
   fs_frame* device_frame() { return frame_; }
-  uint32 samples() const { return samples_; }
+  uint64 samples() const { return samples_; }
   void add_samples(uint32 n) { samples_ += n; }
 
  private:
-  uint32 frame_count_ = 0, width_, height_, samples_ = 0;
+  uint32 frame_count_ = 0, width_, height_;
+  uint64 samples_ = 0;
   fs_frame* frame_ = nullptr;
   std::vector<uint8> display_;
   std::vector<float32> color_;
@@ -378,6 +379,18 @@ void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uin
 float32 TraceRange(const Camera& view, Scene* scene, DisplayFrame* frame, float32 x, float32 y);
 // Device used by TraceScene (default 0); must be called before the first trace.
 bool SetTraceDevice(int device);
+// Mirror-only settings (no reference counterpart): the device context's
+// fs_options, whether large meshes build their BVH on the device (default
+// true; frames are identical either way), and whether each TraceScene call
+// prints the reference's per-frame timing line (engine.cpp:284-293; default
+// off). Scene-build fields apply from the next upload.
+struct TraceSettings {
+  fs_options options;
+  bool device_bvh = true;
+  bool timing_log = false;
+};
+TraceSettings GetTraceSettings();
+bool SetTraceSettings(const TraceSettings& s);
 // fs_status of the last engine call and its message.
 int LastTraceStatus();
 const char* LastTraceError();

@@ -10,7 +10,7 @@
  *
  * which adds ONE jittered sample per pixel to a running-mean frame
  * (engine.cpp:253-296, frame.cpp:53-85). The repo's C++ mirror of that API
- * (final-stage-path-tracer-2-0_amd/host/engine.h) calls the functions below.
+ * (final-stage-path-tracer-2-0_amd/host/fs_host.h) calls the functions below.
  *
  * Conventions: plain C types only; every function returns 0 on success and a
  * negative fs_status on failure (fs_last_error() has the message); no C++
@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 1
+#define FS_ABI_VERSION 2
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -204,12 +204,50 @@ typedef struct fs_counters {
 typedef struct fs_context fs_context;
 typedef struct fs_frame fs_frame;
 
+/*
+ * Tuning options of a context (no reference counterpart: the reference has
+ * one CPU schedule). Every schedule and setting renders identical frames;
+ * they change speed only. The library reads no environment
+ * variables: a context uses fs_options_default() until fs_set_options.
+ */
+typedef enum fs_schedule {
+  FS_SCHEDULE_AUTO = 0,   /* PARKED when the scene has a mesh of >= park_min_tris
+                             triangles and no texture, else LEAN */
+  FS_SCHEDULE_LEAN = 1,   /* path-regeneration megakernel, pooled (pixel, sample) tasks */
+  FS_SCHEDULE_PARKED = 2  /* LEAN + BVH walks of large meshes park when few lanes walk */
+} fs_schedule;
+
+#define FS_NODE_LAYOUT_DEPTH_FIRST 0u
+#define FS_NODE_LAYOUT_PAIRS 1u
+
+typedef struct fs_options {
+  int32_t schedule;            /* fs_schedule (AUTO) */
+  uint32_t park_lanes;         /* PARKED: park when at most this many lanes still walk (10) */
+  uint32_t park_min_tris;      /* meshes whose walks may park (2^19); read at upload */
+  uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (64) */
+  uint32_t groups;             /* sample groups per launch; 0 = sized to >= 262144 blocks (0) */
+  uint32_t group_major;        /* block order: 0 a tile's groups together (0), 1 group by group */
+  uint32_t tile_order;         /* 1 centre-first dispatch of owned tiles (1), 0 index order */
+  uint32_t xcd_bands;          /* 2 whole 64x64 tiles per XCD (2), 1 one band per XCD, 0 none */
+  uint32_t gpu_bvh_min_tris;   /* FS_UPLOAD_GPU_BVH: meshes this large build on the device
+                                  (65536; never below 1024) */
+  uint32_t bvh_leaf;           /* faces per BVH leaf, 1..127 (2) */
+  uint32_t bvh_bins;           /* SAH bins per axis, 2..64 (16) */
+  uint32_t bvh_threads;        /* host BVH build threads, 0 = 16 (0) */
+  uint32_t node_layout;        /* FS_NODE_LAYOUT_* of host-built trees (DEPTH_FIRST) */
+  uint32_t build_log;          /* 1: scene build phases to stderr (0) */
+} fs_options;
+
 /* ---- context ---------------------------------------------------------- */
 int fs_abi_version(void);
 const char* fs_last_error(void);                  /* thread-local message */
 int fs_device_count(int* count);
 int fs_create(int device, fs_context** out);
 int fs_destroy(fs_context* ctx);
+int fs_options_default(fs_options* out);
+/* Applies to later uploads (build fields) and renders (the rest). */
+int fs_set_options(fs_context* ctx, const fs_options* opt);
+int fs_get_options(fs_context* ctx, fs_options* out);
 
 /* Copies the scene, builds per-mesh BVHs on the host and uploads SoA arrays.
  * Replaces any scene previously uploaded to ctx. */
@@ -217,8 +255,8 @@ int fs_upload_scene(fs_context* ctx, const fs_scene_desc* desc);
 /* fs_upload_scene with options. FS_UPLOAD_GPU_BVH builds the BVH of every
  * mesh of >= 65536 triangles on the device (binned SAH, same tree rules as
  * the host build; the frames are identical). fs_upload_scene
- * behaves as flags = 0 unless the environment sets FS_GPU_BVH=1. Replaces
- * the reference's load-time octree build, mesh.cpp:117-152. */
+ * is flags = 0. Replaces the reference's load-time octree build,
+ * mesh.cpp:117-152. */
 #define FS_UPLOAD_GPU_BVH 1u
 int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flags);
 /* Scene build (host preparation + any device BVH build) and upload time of
@@ -266,11 +304,25 @@ int fs_frame_gather(fs_context* ctx, fs_frame* frame,
                     const fs_render_params* params, int root);
 int fs_comm_destroy(fs_context* ctx);
 
+/* The tile exchange of fs_frame_gather without RCCL, through host memory
+ * (tests and tools: an N-rank gather emulated on one device). params' tiling
+ * is tile_offset = rank, tile_stride = nranks. fs_frame_pack writes the
+ * rank's owned tiles (40 B per pixel, fs_frame_pack_bytes per rank);
+ * fs_frame_unpack takes nranks packs concatenated in rank order, as
+ * ncclGather delivers them, and scatters every rank's but its own
+ * (tile_offset) into frame, rebuilding the display bytes. */
+int fs_frame_pack_bytes(const fs_render_params* params, uint64_t* bytes);
+int fs_frame_pack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, void* host_dst, size_t bytes);
+int fs_frame_unpack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, const void* host_src,
+                    size_t bytes);
+
 /* Host only (no device needed): runs the scene preparation of
- * fs_upload_scene (object constructors, BVH build) and returns a 64-bit
- * digest of every array it would upload, the BVH node count and the build
- * time. For build reproducibility checks and load-time measurements. */
-int fs_prepare_digest(const fs_scene_desc* desc, uint64_t* digest, uint64_t* num_nodes, double* build_ms);
+ * fs_upload_scene (object constructors, host BVH build, with the build
+ * fields of opt, NULL = defaults) and returns a 64-bit digest of every array
+ * it would upload, the BVH node count and the build time. For build
+ * reproducibility checks and load-time measurements. */
+int fs_prepare_digest(const fs_scene_desc* desc, const fs_options* opt, uint64_t* digest, uint64_t* num_nodes,
+                      double* build_ms);
 
 /* ---- TraceRange (engine.cpp:298-329) ------------------------------------
  * Focus pick: for each of `count` image points (x, y interleaved in xy) of a

@@ -12,6 +12,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -456,6 +457,10 @@ static inline uint32_t closest_child(const onode* n, v3 p) {
 typedef struct tstats { uint64_t nodes, tris, segs; } tstats;
 static int mesh_node_trace(const omesh* m, uint32_t ni, const ray_t* r, mcoll_t* h, tstats* st);
 
+/* Diagnostics: when set, the octree walk logs its decisions to stderr. */
+static int g_walk_log = 0;
+void oracle_set_walk_log(int on) { g_walk_log = on; }
+
 /* bvh.h:154-231 */
 static int trace_internal(const omesh* m, uint32_t ni, coll_t node_hit, const ray_t* r, mcoll_t* h, tstats* st) {
   const onode* n = &m->nodes[ni];
@@ -476,6 +481,9 @@ static int trace_internal(const omesh* m, uint32_t ni, coll_t node_hit, const ra
     zh = ray_plane(n->split[2], r, &zi);
     if (!xh && !yh && !zh) return mesh_node_trace(m, (uint32_t)n->child[cn], r, h, st);
   }
+  if (g_walk_log)
+    fprintf(stderr, "internal %u depth %u start_in=%d cn=%u x(%d %.9g) y(%d %.9g) z(%d %.9g)\n", ni, n->depth,
+            point_in_bounds(&n->aabb, r->start), cn, xh, xi.param, yh, yi.param, zh, zi.param);
   for (uint32_t i = 0; i < 4; i++) {
     if (mesh_node_trace(m, (uint32_t)n->child[cn], r, h, st)) {
       result = 1;
@@ -500,7 +508,15 @@ static int mesh_node_trace(const omesh* m, uint32_t ni, const ray_t* r, mcoll_t*
   const onode* n = &m->nodes[ni];
   coll_t nh = no_coll();
   if (st) st->nodes++;
-  if (!ray_bounds(&n->aabb, r, &nh) || nh.param > h->param) return 0;
+  if (!ray_bounds(&n->aabb, r, &nh) || nh.param > h->param) {
+    if (g_walk_log)
+      fprintf(stderr, "  node %u culled (param %.9g best %.9g start_in %d)\n", ni, nh.param, h->param,
+              point_in_bounds(&n->aabb, r->start));
+    return 0;
+  }
+  if (g_walk_log)
+    fprintf(stderr, "  node %u visit leaf=%d nfaces=%u param %.9g box [%g %g %g]-[%g %g %g]\n", ni, n->leaf,
+            n->nfaces, nh.param, n->aabb.mn.x, n->aabb.mn.y, n->aabb.mn.z, n->aabb.mx.x, n->aabb.mx.y, n->aabb.mx.z);
   int result = 0;
   if (n->leaf) {
     for (uint32_t i = 0; i < n->nfaces; i++) {
@@ -1013,6 +1029,11 @@ static v3 sample_sky(const oracle_scene* sc, v3 view) {
 /* ------------------------------------------------------------------------ */
 typedef struct tresult { v3 color, normal; float depth; uint64_t material_id; uint64_t ray_count; } tresult; /* frame.h:40-47 */
 
+/* Diagnostics: when set, trace_step records each segment (start, stop, dir,
+ * closest-hit param) here (oracle_trace_path; single-threaded use only). */
+static float* g_seg_rec = NULL;
+static uint32_t g_seg_n = 0, g_seg_max = 0;
+
 static v3 trace_step(const oracle_scene* sc, const fs_camera* cam, const ray_t* r, v3* hit_position, uint32_t depth,
                      tresult* res, uint64_t* rng, tstats* st) {
   if (depth >= K_TRACE_DEPTH) return mk3(0, 0, 0);
@@ -1020,7 +1041,15 @@ static v3 trace_step(const oracle_scene* sc, const fs_camera* cam, const ray_t* 
   res->ray_count = depth + 1;
   ocoll ci;
   if (st) st->segs++;
-  if (!scene_trace(sc, r, &ci, st)) {
+  const int det = scene_trace(sc, r, &ci, st);
+  if (g_seg_rec && g_seg_n < g_seg_max) {
+    float* q = g_seg_rec + 10 * g_seg_n++;
+    q[0] = r->start.x; q[1] = r->start.y; q[2] = r->start.z;
+    q[3] = r->stop.x; q[4] = r->stop.y; q[5] = r->stop.z;
+    q[6] = r->dir.x; q[7] = r->dir.y; q[8] = r->dir.z;
+    q[9] = det ? ci.param : 2.0f;
+  }
+  if (!det) {
     if (hit_position) *hit_position = r->stop;
     v3 out = sample_sky(sc, norm3(sub3(r->stop, r->start)));
     if (depth == 0) {
@@ -1356,4 +1385,90 @@ int oracle_ray_triangle(const float* p1, const float* p2, const float* p3, const
 int oracle_triangle_box(const float* p1, const float* p2, const float* p3, const float* mn, const float* mx) {
   bounds_t b; b.mn = mk3(mn[0], mn[1], mn[2]); b.mx = mk3(mx[0], mx[1], mx[2]); b.count = 2;
   return tri_vs_bounds(mk3(p1[0], p1[1], p1[2]), mk3(p2[0], p2[1], p2[2]), mk3(p3[0], p3[1], p3[2]), &b);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Diagnostics (tests/tools): the camera ray of one sample, and one object's  */
+/* closest hit on a segment, through the octree or over every face.           */
+/* ------------------------------------------------------------------------ */
+int oracle_camera_ray(const fs_camera* cam, uint32_t W, uint32_t H, uint32_t x, uint32_t y, uint32_t sample,
+                      uint64_t seed, float* start, float* stop) {
+  cambasis b;
+  camera_basis(cam, W, H, &b);
+  uint64_t rng = oracle_pixel_seed((uint64_t)y * W + x, sample, seed);
+  ray_t r = camera_ray(cam, &b, (float)x, (float)y, &rng);
+  start[0] = r.start.x; start[1] = r.start.y; start[2] = r.start.z;
+  stop[0] = r.stop.x; stop[1] = r.stop.y; stop[2] = r.stop.z;
+  return 0;
+}
+
+int oracle_trace_path(const oracle_scene* sc, const fs_camera* cam, uint32_t W, uint32_t H, uint32_t x, uint32_t y,
+                      uint32_t sample, uint64_t seed, float* segs, uint32_t max) {
+  cambasis b;
+  camera_basis(cam, W, H, &b);
+  tresult res;
+  g_seg_rec = segs;
+  g_seg_n = 0;
+  g_seg_max = max;
+  trace_pixel_sample(sc, cam, &b, W, x, y, sample, seed, &res, NULL);
+  g_seg_rec = NULL;
+  return (int)g_seg_n;
+}
+
+int oracle_object_trace(const oracle_scene* sc, uint32_t obj, const float* s, const float* e, const float* dir,
+                        float best, int brute, float* param, uint32_t* face) {
+  if (obj >= sc->nobjs) return FS_ERR_INVALID;
+  const oobj* o = &sc->objs[obj];
+  ray_t r = mkray(mk3(s[0], s[1], s[2]), mk3(e[0], e[1], e[2]));
+  r.dir = mk3(dir[0], dir[1], dir[2]);
+  *face = 0xFFFFFFFFu;
+  *param = best;
+  if (o->kind != FS_OBJ_MESH || !brute) {
+    ocoll h;
+    memset(&h, 0, sizeof(h));
+    h.param = best;
+    if (o->kind == FS_OBJ_MESH) {
+      const omesh* m = &sc->meshes[o->mesh];
+      mcoll_t mc;
+      mc.param = best; mc.point = mk3(0, 0, 0); mc.normal = mk3(0, 0, 0); mc.face = 0xFFFFFFFFu; mc.bu = mc.bv = 0;
+      if (m->has_tree && mesh_node_trace(m, 0, &r, &mc, NULL)) { *param = mc.param; *face = mc.face; return 1; }
+      return 0;
+    }
+    if (object_trace(sc, o, &r, &h, NULL)) { *param = h.param; return 1; }
+    return 0;
+  }
+  const omesh* m = &sc->meshes[o->mesh];
+  int hit = 0;
+  for (uint32_t f = 0; f < m->nf; f++) {
+    const oface* fc = &m->faces[f];
+    coll_t th = no_coll();
+    float bu, bv;
+    if (ray_tri(m->verts[fc->vi[0]], m->verts[fc->vi[1]], m->verts[fc->vi[2]], fc->plane, &r, &th, &bu, &bv) &&
+        th.param < *param) {
+      *param = th.param; *face = f; hit = 1;
+    }
+  }
+  return hit;
+}
+
+/* Which octree leaves hold face f of mesh m, and the leaf boxes (up to max). */
+int oracle_face_leaves(const oracle_scene* sc, uint32_t mesh, uint32_t f, uint32_t* leaves, float* boxes, uint32_t max) {
+  if (mesh >= sc->nmeshes) return -1;
+  const omesh* m = &sc->meshes[mesh];
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < m->nnodes; i++) {
+    const onode* nd = &m->nodes[i];
+    if (!nd->leaf) continue;
+    for (uint32_t j = 0; j < nd->nfaces; j++)
+      if (nd->faces[j] == f) {
+        if (n < max) {
+          leaves[n] = i;
+          float* b = boxes + 6 * n;
+          b[0] = nd->aabb.mn.x; b[1] = nd->aabb.mn.y; b[2] = nd->aabb.mn.z;
+          b[3] = nd->aabb.mx.x; b[4] = nd->aabb.mx.y; b[5] = nd->aabb.mx.z;
+        }
+        n++;
+      }
+  }
+  return (int)n;
 }

@@ -72,6 +72,27 @@ int oracle_trace_range(const oracle_scene* scene, const fs_camera* camera,
                        uint32_t width, uint32_t height, float x, float y,
                        float* distance);
 
+/* ---- diagnostics (tests/tools) ------------------------------------------- */
+/* The camera ray (engine.cpp:210-244) of sample `sample` of pixel (x, y). */
+int oracle_camera_ray(const fs_camera* camera, uint32_t width, uint32_t height, uint32_t x, uint32_t y,
+                      uint32_t sample, uint64_t seed, float start[3], float stop[3]);
+/* The segments TraceStep traces for one sample: 10 floats each (start,
+ * stop, dir, closest-hit param or 2); returns their number (<= max). */
+int oracle_trace_path(const oracle_scene* scene, const fs_camera* camera, uint32_t width, uint32_t height,
+                      uint32_t x, uint32_t y, uint32_t sample, uint64_t seed, float* segs, uint32_t max);
+/* Object `obj`'s closest hit on the segment (start, stop, dir) with param
+ * pre-seeded by `best` (Object::Trace; meshes through the octree, or over
+ * every face when brute != 0). Returns 1 on a hit; *face is the mesh face or ~0u. */
+int oracle_object_trace(const oracle_scene* scene, uint32_t obj, const float start[3], const float stop[3],
+                        const float dir[3], float best, int brute, float* param, uint32_t* face);
+/* The octree leaves of mesh `mesh` that list face f (node ids and boxes,
+ * up to max); returns how many there are. */
+int oracle_face_leaves(const oracle_scene* scene, uint32_t mesh, uint32_t f, uint32_t* leaves, float* boxes,
+                       uint32_t max);
+
+/* Logs the octree walk's decisions to stderr while on (not thread-safe). */
+void oracle_set_walk_log(int on);
+
 /* ---- known-answer helpers ---------------------------------------------- */
 uint64_t oracle_splitmix64(uint64_t x);
 uint64_t oracle_pixel_seed(uint64_t pixel, uint64_t sample, uint64_t seed);

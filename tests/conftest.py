@@ -50,7 +50,7 @@ def load_scene(name, scene_dir):
 
 
 @pytest.fixture(scope="session")
-def gpu_renderer():
+def _session_renderer():
     import fsamd
 
     if fsamd.device_count() < 1:
@@ -58,3 +58,12 @@ def gpu_renderer():
     r = fsamd.Renderer(0)
     yield r
     r.close()
+
+
+@pytest.fixture
+def gpu_renderer(_session_renderer):
+    """The session's fs_context, back on fs_options_default() after each test."""
+    import fsamd
+
+    yield _session_renderer
+    _session_renderer.set_options(**fsamd.options_dict(fsamd.options()))

@@ -45,12 +45,12 @@ def assert_oracle(out, desc_ptr, cam, W, H, spp):
 
 
 @pytest.mark.parametrize("name,dims,min_tris", [("c4", (1920, 1080, 4), None), ("c3", (480, 270, 8), "1024")])
-def test_device_bvh_frames_equal_host_bvh(name, dims, min_tris, scene_dir, gpu_renderer, monkeypatch):
+def test_device_bvh_frames_equal_host_bvh(name, dims, min_tris, scene_dir, gpu_renderer):
     """C4 (one 1 M-face mesh: the default threshold defers it) at full 1080p,
     and C3 with the threshold lowered so every mesh of >= 1024 faces takes the
     device build."""
     if min_tris:
-        monkeypatch.setenv("FS_GPU_BVH_MIN_TRIS", min_tris)
+        gpu_renderer.set_options(gpu_bvh_min_tris=int(min_tris))
     W, H, spp = dims
     s = load_scene(name, scene_dir)
     cam = s.camera(0)
@@ -87,13 +87,13 @@ def grid(n, z, jitter=0.0, seed=0):
     return pos, faces, nrm, tex
 
 
-def test_device_bvh_degenerate_and_attributed_meshes(gpu_renderer, monkeypatch):
+def test_device_bvh_degenerate_and_attributed_meshes(gpu_renderer):
     """Edge cases of the device build, each against the host build and the
     oracle: 4096 copies of one triangle (every centroid equal: even splits down
     to the leaf bound, ties broken by face index), a coplanar grid (zero
     extent on one axis) carrying vertex normals and texcoords under a diffuse
     map, and a jittered grid with inverted normals behind it."""
-    monkeypatch.setenv("FS_GPU_BVH_MIN_TRIS", "1024")
+    gpu_renderer.set_options(gpu_bvh_min_tris=1024)
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
     red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))

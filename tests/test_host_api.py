@@ -198,9 +198,8 @@ def test_parallel_bvh_build_is_reproducible(scene_dir, monkeypatch):
 
     s = load_scene("c3", scene_dir)
     digests = set()
-    for threads in ("1", "2", "16"):
-        monkeypatch.setenv("FS_BVH_THREADS", threads)
-        d, nodes, ms = fsamd.prepare_digest(s.desc_ptr())
+    for threads in (1, 2, 16):
+        d, nodes, ms = fsamd.prepare_digest(s.desc_ptr(), bvh_threads=threads)
         digests.add((d, nodes))
     assert len(digests) == 1
 

@@ -4,7 +4,7 @@
 
 Prints one JSON line per (scene, builder) with the median build_ms of
 fs_scene_stats (host preparation + device BVH build) and the node count.
-Set FS_BUILD_LOG=1 for the per-phase split of the device build.
+--log prints the per-phase split of the device build (fs_options.build_log).
 """
 import argparse
 import json
@@ -23,9 +23,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", default="c3,c4")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--log", action="store_true")
     a = ap.parse_args()
     d = tempfile.mkdtemp(prefix="fs_bvht_")
-    r = fsamd.Renderer(0)
+    r = fsamd.Renderer(0, build_log=int(a.log))
     for name in a.scenes.split(","):
         path = scenes.write(name, os.path.join(d, name))
         fsamd.reset_main_rng()

@@ -3,7 +3,7 @@
   python tools/bvh_layout_ab.py [scenes] [spp] [rounds] [variants]
 
 variants: comma list of host|device, each optionally with upload-time env
-settings, e.g. "host,host@FS_NODE_LAYOUT=pairs" (default "host,device").
+fs_options settings, e.g. "host,host@node_layout=pairs" (default "host,device").
 
 Two contexts on one GPU hold the same scene, one uploaded with the host SAH
 build and one with FS_UPLOAD_GPU_BVH; their renders alternate and every frame
@@ -35,19 +35,9 @@ def main():
         cam = s.camera(0)
         ctx = {}
         for b in variants:
-            builder, *extra = b.split("@")
-            saved = {}
-            for kv in extra:
-                k, v = kv.split("=", 1)
-                saved[k] = os.environ.get(k)
-                os.environ[k] = v
-            r = fsamd.Renderer(0)
+            builder, _, extra = b.partition("@")
+            r = fsamd.Renderer(0, **fsamd.parse_variant(extra))
             r.upload(s, gpu_bvh=builder == "device")
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k)
-                else:
-                    os.environ[k] = v
             ctx[b] = (r, r.frame(W, H), r.scene_stats())
         res = {b: [] for b in ctx}
         ref = None

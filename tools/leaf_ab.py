@@ -1,5 +1,5 @@
 """A/B of BVH build settings in one process: rebuild + time.
-usage: python tools/leaf_ab.py VALUES scenes [spp] [ENV]   (ENV default FS_BVH_LEAF; e.g. FS_BVH_BINS)"""
+usage: python tools/leaf_ab.py VALUES scenes [spp] [FIELD]   (fs_options field, default bvh_leaf; e.g. bvh_bins)"""
 import os
 import sys
 import time
@@ -14,7 +14,7 @@ import scenes  # noqa: E402
 leaves = sys.argv[1].split(",")
 names = sys.argv[2].split(",")
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
-env = sys.argv[4] if len(sys.argv) > 4 else "FS_BVH_LEAF"
+env = sys.argv[4] if len(sys.argv) > 4 else "bvh_leaf"
 W, H = 1920, 1080
 for name in names:
     p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
@@ -26,7 +26,7 @@ for name in names:
     f = r.frame(W, H)
     ref = None
     for lf in leaves:
-        os.environ[env] = lf
+        r.set_options(**{env: int(lf)})
         r.upload(s)
         st = r.scene_stats()
         ms = []

@@ -1,7 +1,6 @@
-"""Interleaved A/B of kernel variants (FS_KERNEL env) in one process.
-usage: python tools/perf_ab.py modes scenes [spp] [rounds]
-(modes: lean, regen, lockstep, wavefront — see kernel_mode() in fs_device.hip;
- a variant may set more env vars: "lean_susp@FS_XCD_BANDS=1@FS_SUSP_THR=8")"""
+"""Interleaved A/B of render options (fs_options) in one process.
+usage: python tools/perf_ab.py variants scenes [spp] [rounds]
+(a variant is default or fields joined by @, e.g. "schedule=parked@xcd_bands=1@park_lanes=8")"""
 import os
 import sys
 import time
@@ -34,16 +33,10 @@ def main():
         ref = None
         for rd in range(rounds + 1):
             for v in variants:
-                mode, *extra = v.split("@")
-                os.environ["FS_KERNEL"] = mode
-                for kv in extra:
-                    k, val = kv.split("=", 1)
-                    os.environ[k] = val
+                r.set_options(**fsamd.options_dict(fsamd.options(**fsamd.parse_variant(v))))
                 f.reset()
                 r.render(cam, f, spp=spp)
                 ms = r.last_render_ms()
-                for kv in extra:
-                    os.environ.pop(kv.split("=", 1)[0], None)
                 if rd:
                     res[v].append(ms)
                 img = f.read(fsamd.PLANE_COLOR)

@@ -2,7 +2,7 @@
 share (tile_offset r, tile_stride N) of the bench frame in turn and reports
 the slowest rank's render time per N (gather excluded).
 usage: python tools/scaling_sim.py [scene] [spp] [Ns] [variants]
-(variants: comma list of env settings, e.g. "FS_GROUPS=1,default")"""
+(variants: comma list of fs_options settings, e.g. "groups=1,default"; TS=<n> sets the tile size)"""
 import os
 import sys
 
@@ -28,13 +28,9 @@ def main():
     f = r.frame(W, H)
     r.render(cam, f, spp=64)  # warm up (allocations, caches)
     for v in variants:
-        env = {}
-        if v != "default":
-            for kv in v.split("@"):
-                k, val = kv.split("=", 1)
-                env[k] = val
-        ts = int(env.pop("TS", 64))  # tile size (a render parameter, not an env knob)
-        os.environ.update(env)
+        opts = fsamd.parse_variant(v)
+        ts = int(opts.pop("TS", 64))  # tile size (a render parameter, not an option)
+        r.set_options(**fsamd.options_dict(fsamd.options(**opts)))
         base = None
         for n in ns:
             times = []
@@ -48,8 +44,6 @@ def main():
             base = base or rate
             print(f"{name} {v} N={n}: slowest rank {worst:.1f} ms (mean {sum(times)/n:.1f}), "
                   f"{rate:.0f} Msamples/s, efficiency {rate / base / n:.3f}, launches/rank {launches}", flush=True)
-        for k in env:
-            os.environ.pop(k, None)
     f.close()
     r.close()
 
