@@ -424,9 +424,40 @@ struct Aov {
   uint64_t id;
 };
 
-__device__ __forceinline__ uint32_t mat_of(uint32_t lo, uint32_t hi, int k) {
-  return (k < 4 ? (lo >> (8 * k)) : (hi >> (8 * (k - 4)))) & 0xFFu;
+// base + a 32-bit byte offset: lets the compiler use the SGPR-base + 32-bit
+// VGPR-offset addressing form instead of keeping a 64-bit pointer per lane.
+template <class T>
+__device__ __forceinline__ T* at_byte(T* base, uint32_t off) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
 }
+
+// The material index of every bounce of a path, for the backward pass. Up to
+// 255 materials: 8-bit ids packed in two registers. More (MMAT): one u32 per
+// bounce in a per-lane scratch row ([level][lane] per wave), so scenes with
+// any number of materials render (scene.cpp:251-310 has no limit) and the
+// common case keeps its registers.
+template <bool MMAT>
+struct MatTrail {
+  uint32_t lo = 0, hi = 0;
+  uint32_t* row = nullptr;  // MMAT: the wave's row base
+  uint32_t lane = 0;
+  __device__ __forceinline__ void reset() { lo = hi = 0; }
+  __device__ __forceinline__ void set(uint32_t k, uint32_t mi) {
+    if (MMAT) {
+      *at_byte(row, (k * kBlock + lane) * 4u) = mi;
+      if (k == 0) lo = mi;
+    } else if (k < 4) {
+      lo |= mi << (8 * k);
+    } else {
+      hi |= mi << (8 * (k - 4));
+    }
+  }
+  __device__ __forceinline__ uint32_t get(int k) const {
+    if (MMAT) return k == 0 ? lo : *at_byte(row, ((uint32_t)k * kBlock + lane) * 4u);
+    return (k < 4 ? (lo >> (8 * k)) : (hi >> (8 * (k - 4)))) & 0xFFu;
+  }
+};
 
 // engine.cpp:210-244: jittered ray through the pixel, optional thin lens.
 __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy, uint64_t& rng) {
@@ -459,23 +490,16 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
 // engine.cpp:210-244. Returns the TraceResult colour.
 // Backward pass: Material::Sample in the order the TraceStep recursion
 // returns (engine.cpp:141-156); L enters as the radiance of level `top`+1.
-// base + a 32-bit byte offset: lets the compiler use the SGPR-base + 32-bit
-// VGPR-offset addressing form instead of keeping a 64-bit pointer per lane.
-template <class T>
-__device__ __forceinline__ T* at_byte(T* base, uint32_t off) {
-  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
-  return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
-}
 
 // texrow: per-level SampleDiffuse result of a textured material (lean kernel
 // only; other schedules pass nullptr and never see a textured scene).
-template <bool TEX = false>
-__device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t mats_lo, uint32_t mats_hi,
+template <bool TEX = false, bool MMAT = false>
+__device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const MatTrail<MMAT>& mats,
                                      const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
                                      int stride = kBlock, uint32_t lane = 0,
                                      const float4* __restrict__ texrow = nullptr) {
   for (int k = top; k >= 0; --k) {
-    const fs_material& m = S.materials[mat_of(mats_lo, mats_hi, k)];
+    const fs_material& m = S.materials[mats.get(k)];
     float2 cs = *at_byte(lvl, ((uint32_t)k * (uint32_t)stride + lane) * 8u);
     f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
     f3 sd = dif;  // SampleDiffuse (material.cpp:108-126)
@@ -520,7 +544,7 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, uint32_t 
     }
   }
   if (top >= 0) {  // engine.cpp:147-151
-    const fs_material& m0 = S.materials[mat_of(mats_lo, mats_hi, 0)];
+    const fs_material& m0 = S.materials[mats.get(0)];
     if (length(L) > 10.0f && m0.kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
   }
   return L;
@@ -1054,12 +1078,13 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false>
+template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
                                                                      float4* __restrict__ tex_all,
                                                                      float* __restrict__ rad_all,
+                                                                     uint32_t* __restrict__ mat_all,
                                                                      DevCounters* __restrict__ counters) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
   const uint32_t lane = threadIdx.x;
@@ -1130,7 +1155,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   uint32_t s = 0;
   uint64_t rng = 0;
   Ray r;
-  uint32_t depth = 0, mats_lo = 0, mats_hi = 0;
+  uint32_t depth = 0;
+  MatTrail<MMAT> mats;
+  mats.row = MMAT ? mat_all + (size_t)blockIdx.x * (kMaxDepth * kBlock) : nullptr;
+  mats.lane = lane;
   int top = -1;
   bool fresh = true;
   MinHit h;         // persists across iterations while a walk is parked (SUSP)
@@ -1170,7 +1198,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       rng = pixel_seed(pix, sample_base + s, P.seed);
       r = camera_ray(C, (float)x, (float)y, rng);
       depth = 0;
-      mats_lo = mats_hi = 0;
+      mats.reset();
       top = -1;
       *at_byte(anchor, a0_off) = make_float4(0, 0, 0, 0);
       *at_byte(anchor, a1_off) = make_float4(0, 0, 0, 0);
@@ -1262,10 +1290,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           ds = pow50(dot(hv, nn));
         }
         *at_byte(lvl, (depth * kBlock + lane) * 8u) = make_float2(c, ds);
-        if (depth < 4)
-          mats_lo |= (uint32_t)mi << (8 * depth);
-        else
-          mats_hi |= (uint32_t)mi << (8 * (depth - 4));
+        mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
         if (depth == 0 && last_group && s == P.spp - 1) {
@@ -1293,12 +1318,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     FS_PHASE(3);
     if (done) {
       f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-      if (top >= 0 && S.materials[mats_lo & 0xFFu].kind == FS_MAT_FOG) {
+      if (top >= 0 && S.materials[mats.get(0)].kind == FS_MAT_FOG) {
         float4 a = *at_byte(anchor, a0_off), b = *at_byte(anchor, a1_off);
         p0 = mk3(a.x, a.y, a.z);
         lp0 = mk3(b.x, b.y, b.z);
       }
-      L = unwind<TEX>(S, L, top, mats_lo, mats_hi, lvl, p0, lp0, rng, kBlock, lane, texrow);
+      L = unwind<TEX, MMAT>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
       const uint32_t o = s * kBlock + task_lp;
       rad[o] = L.x;
       rad[kChunk * kBlock + o] = L.y;
@@ -1526,6 +1551,7 @@ struct fs_context {
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= park_min_tris triangles: the PARKED schedule
+  bool many_materials = false;  // > kPackedMaterials: material ids in scratch rows (MMAT kernels)
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
   std::vector<uint32_t> tile_order_host;  // the device tile_order buffer holds this order of ...
   uint64_t tile_order_key[3] = {0, 0, 0};  // ... the tile set (offset, stride, owned; width, height) it was built for
@@ -1620,10 +1646,11 @@ struct LeanRows {
   float4* anchor = nullptr;
   float4* tex = nullptr;
   float* rad = nullptr;
+  uint32_t* mat = nullptr;
 };
-int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows) {
-  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk;
-  const size_t bytes = (size_t)slots * per + 4 * 256;  // + alignment of each array
+int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows, bool mat_rows) {
+  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk + (mat_rows ? 4 * kMaxDepth : 0);
+  const size_t bytes = (size_t)slots * per + 5 * 256;  // + alignment of each array
   if (ctx->rows.bytes < bytes) {
     int rc = ensure(&ctx->rows, bytes);
     if (rc) return rc;
@@ -1639,6 +1666,7 @@ int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows) {
   W->lvl = (float2*)take(8ull * kMaxDepth * slots);
   W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
   W->rad = (float*)take(12ull * kChunk * slots);
+  W->mat = mat_rows ? (uint32_t*)take(4ull * kMaxDepth * slots) : nullptr;
   if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
   return FS_OK;
 }
@@ -1704,6 +1732,31 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #endif
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
+
+// The instantiations of the lean kernel: <COUNT, waves, TEX, SUSP (parked
+// walks), MMAT (material ids in scratch rows)>. Textured scenes never park.
+// Names as rocprofv3 prints the uncounted ones (fs_last_kernel).
+typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, float2*, float4*, float4*, float*, uint32_t*,
+                       DevCounters*);
+struct LeanKernel {
+  LeanFn fn;
+  const char* name;
+};
+template <bool TEX, bool SUSP, bool MMAT>
+LeanKernel lean_kernel(bool count) {
+  constexpr int W = SUSP ? FS_SUSP_WAVES : FS_LEAN_WAVES;
+  static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
+                                  (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
+                                  (MMAT ? "true" : "false") + ">";
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT>,
+          name.c_str()};
+}
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials) {
+  if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
+  if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
+  return many_materials ? lean_kernel<false, false, true>(count) : lean_kernel<false, false, false>(count);
+}
 
 bool valid_options(const fs_options* o, std::string* why) {
   if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_PARKED) *why = "unknown schedule";
@@ -1818,7 +1871,6 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   const BuildOptions bo = BuildOptions::from(&ctx->opt);
   int rc = prepare_scene(desc, &P, &err, bo, gpu_min);
   if (rc) return fail(rc, err);
-  if (P.materials.size() > 255) return fail(FS_ERR_INVALID, "at most 255 materials are supported");
   if ((rc = set_device(ctx))) return rc;
   auto t0 = std::chrono::steady_clock::now();
   ctx->have_scene = false;
@@ -1897,6 +1949,7 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   for (const fs_material& m : P.materials) ctx->has_textures |= m.texture >= 0;
   ctx->has_parking = false;
   for (const DevObject& o : P.objects) ctx->has_parking |= o.kind == FS_OBJ_MESH && o.i5 != 0;
+  ctx->many_materials = P.materials.size() > kPackedMaterials;
   ctx->num_objects = S.num_objects;
   ctx->host = std::move(P);
   ctx->have_scene = true;
@@ -2074,18 +2127,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
   LeanRows rows;
-  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures))) return rc;
-  // (names as rocprofv3 prints the uncounted instantiations, for fs_last_kernel)
-  auto lk = count ? dev::render_kernel_lean<true, 6, false, false> : dev::render_kernel_lean<false, FS_LEAN_WAVES, false, false>;
-  ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_LEAN_WAVES) ", false, false>";
-  if (ctx->has_textures) {  // textured scenes: the instantiation with texcoords + texel rows
-    lk = count ? dev::render_kernel_lean<true, 6, true, false> : dev::render_kernel_lean<false, 6, true, false>;
-    ctx->last_kernel = "render_kernel_lean<false, 6, true, false>";
-  } else if (parked) {
-    lk = count ? dev::render_kernel_lean<true, 6, false, true>
-               : dev::render_kernel_lean<false, FS_SUSP_WAVES, false, true>;
-    ctx->last_kernel = "render_kernel_lean<false, " FS_STR(FS_SUSP_WAVES) ", false, true>";
-  }
+  const bool mm = ctx->many_materials;
+  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures, mm))) return rc;
+  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm);
+  ctx->last_kernel = K.name;
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
@@ -2093,8 +2138,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     done += L.groups * L.spp;
     ctx->last_launches++;
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
-    hipLaunchKernelGGL(lk, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
-                       rows.lvl, rows.anchor, rows.tex, rows.rad, (DevCounters*)ctx->counters.p);
+    hipLaunchKernelGGL(K.fn, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
+                       rows.lvl, rows.anchor, rows.tex, rows.rad, rows.mat, (DevCounters*)ctx->counters.p);
     if (L.groups > 1)
       hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
     FS_HIP(hipGetLastError());

@@ -19,6 +19,9 @@ constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS col
 #define FS_CHUNK 64  // C4 +1.5 % over 32 (shorter task-pool tails per block), 16 -2 %
 #endif
 constexpr uint32_t kChunk = FS_CHUNK;  // samples per pixel per block (fs_render splits longer renders)
+// Scenes with at most this many materials pack a path's per-bounce material
+// ids in two registers (8 bits each); larger ones use a scratch row (MMAT).
+constexpr uint32_t kPackedMaterials = 255;
 // fs_render sizes sample groups so one launch holds at least this many blocks
 // (~43 per wave slot of 256 CUs x 24 waves; C4 1080p x 1024 spp: 2 launches
 // of 512 spp, +2.6 % over 4 launches of 256 — a launch ends with a tail of

@@ -81,7 +81,7 @@ def test_scene_parity(name, dims, scene_dir, gpu_renderer):
     out = gpu_render(gpu_renderer, s, s.camera(0), W, H, spp)
     # only C4 has a mesh large enough (>= 2^19 triangles) for parked walks
     k = gpu_renderer.last_kernel()
-    parked = k.startswith("render_kernel_lean<false, ") and k.endswith(", false, true>")
+    parked = k.startswith("render_kernel_lean<false, ") and k[:-1].split(", ")[3] == "true"  # <.., waves, TEX, SUSP, MMAT>
     assert parked == (name == "c4"), gpu_renderer.last_kernel()
     ref = oracle_render(s.desc_ptr(), s.camera(0), W, H, spp)
     assert_parity(out, ref, exact=True)
@@ -629,3 +629,60 @@ def test_bench_scale_parity(name, schedule, scene_dir, gpu_renderer):
     assert_parity(out, ref, exact=False)
     for p in (fsamd.PLANE_MATERIAL, fsamd.PLANE_NORMAL, fsamd.PLANE_DEPTH):  # the last sample's AOVs
         assert diff[p] <= 1e-3 * W * H, diff
+
+
+# ---- scenes with more than 255 materials (material ids in scratch rows) ----
+def many_material_scene(textured=False):
+    """A Cornell room plus 64 spheres and cuboids whose 300+ materials cycle
+    through every kind; objects use ids above 255 as well as below."""
+    b = DescBuilder()
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(15, 15, 15))
+    cornell_room(b, white, red, light)
+    tex = b.texture(np.random.default_rng(5).random((8, 12, 3), dtype=np.float32)) if textured else -1
+    rng = np.random.default_rng(11)
+    kinds = [fsamd.MAT_DIFFUSE, fsamd.MAT_METAL, fsamd.MAT_CERAMIC, fsamd.MAT_GLASS, fsamd.MAT_MIRROR,
+             fsamd.MAT_LIQUID, fsamd.MAT_GLOW, fsamd.MAT_LIGHT, fsamd.MAT_FOG]
+    mats = []
+    for i in range(300):
+        k = kinds[i % len(kinds)]
+        c = tuple(float(v) for v in rng.uniform(0.2, 0.95, 3))
+        kw = {}
+        if k == fsamd.MAT_LIGHT:
+            kw["emissive"] = tuple(3 * v for v in c)
+        if k == fsamd.MAT_GLOW:
+            kw["glow"] = tuple(0.2 * v for v in c)
+        if k == fsamd.MAT_FOG:
+            kw["density"] = 0.05
+        if textured and i % 5 == 0 and k in (fsamd.MAT_DIFFUSE, fsamd.MAT_METAL, fsamd.MAT_CERAMIC):
+            kw.update(texture=tex, texture_scale=1.5)
+        mats.append(b.material(k, diffuse=c, roughness=float(rng.uniform(0, 1)), shininess=0.6, index=0.7,
+                               reflectivity=0.2, **kw))
+    assert len(b.mats) > 300
+    for j in range(64):
+        m = mats[(37 * j + 250) % len(mats)]
+        x, y, z = rng.uniform(-8, 8), rng.uniform(1, 18), rng.uniform(-8, 8)
+        if j % 2:
+            b.obj(fsamd.OBJ_SPHERE, m, [x, y, z, float(rng.uniform(0.5, 1.5))])
+        else:
+            b.obj(fsamd.OBJ_CUBOID, m, [x, y, z, 1.5, 1.0, 2.0, 0.3, 1.0, 0.2, 0.7], rotate=1)
+    return b
+
+
+@pytest.mark.parametrize("variant", ["lean", "parked", "textured"])
+def test_many_materials_bit_exact(variant, gpu_renderer):
+    """Scenes with > 255 materials (the reference keeps any number,
+    scene.cpp:251-310) take the kernels that keep per-bounce material ids in
+    a scratch row; bit-exact with the oracle on the lean, parked and
+    textured instantiations."""
+    b = many_material_scene(textured=variant == "textured")
+    ptr = b.build()
+    if variant == "parked":
+        gpu_renderer.set_options(schedule="parked", park_min_tris=1)
+    out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    k = gpu_renderer.last_kernel()
+    assert k.endswith(", true>"), k  # the MMAT instantiation
+    assert (k[:-1].split(", ")[3] == "true") == (variant == "parked"), k
+    ref = oracle_render(ptr, CAM, 96, 72, 16)
+    assert_parity(out, ref, exact=True)
