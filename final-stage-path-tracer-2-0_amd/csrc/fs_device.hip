@@ -143,6 +143,24 @@ __device__ __forceinline__ bool ref_ray_bounds(f3 mn, f3 mx, const Ray& r, bool 
   return true;
 }
 
+// ray_intersect_bounds with its collision point (intersect.cpp:599-654): the
+// point is start + (stop - start) * t of the (possibly reversed) segment.
+__device__ __forceinline__ bool ref_bounds_hit(f3 mn, f3 mx, const Ray& r, bool zl, float& param, f3& point) {
+  const bool si = in_bounds(mn, mx, r.start);
+  if (zl || (si && in_bounds(mn, mx, r.stop))) {
+    if (!si) return false;
+    param = 0.0f;
+    point = r.start;
+    return true;
+  }
+  const f3 a = si ? r.stop : r.start, b = si ? r.start : r.stop;
+  float t;
+  if (!ref_bounds_worker(mn, mx, a, b, t)) return false;
+  point = a + (b - a) * t;
+  param = si ? 1.0f - t : t;
+  return true;
+}
+
 // The mesh-root cull of MeshBvhNode::Trace (mesh.cpp:79-83): true when the
 // reference would NOT skip the mesh (ray_intersect_bounds hits and its param
 // is <= best). Slab times use v_rcp (relative error < 3e-7 against the
@@ -798,14 +816,193 @@ struct PhaseAcc {};
 #define FS_TICK() 0ull
 #endif
 
+// ---- the scene object octree (SceneBvh, scene.cpp:11-133) -----------------
+// One object's Object::Trace into the hit record h (per-lane object index;
+// meshes pre-seeded with h.t, mesh.cpp:277-281). Returns true when the
+// object wrote h (it then holds the object's hit).
+template <bool COUNT, bool TEX>
+__device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, const Ray& r, bool zl, MinHit& h,
+                                             uint32_t* __restrict__ stk, Tally<COUNT>& tally, const Slopes* slp) {
+  const DevObject* __restrict__ o = S.objects + oi;
+  const float* d = o->d;
+  const int32_t kind = o->kind;
+  if (kind == FS_OBJ_MESH) {
+    if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) return false;
+    const int32_t before = h.obj;
+    traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+    const bool wrote = h.obj == (int32_t)oi && before != (int32_t)oi;
+    if (TEX && wrote && o->i4) h.tc = (int32_t)oi;  // mesh.cpp:300-311: only with texcoords
+    return wrote;
+  }
+  if (zl) return false;
+  if (COUNT) tally.prims++;
+  float t;
+  f3 p, n;
+  bool hit = false;
+  if (kind == FS_OBJ_SPHERE) {
+    hit = ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n) && t < h.t;
+  } else if (kind == FS_OBJ_PLANE) {
+    hit = ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p) && t < h.t;
+  } else if (kind == FS_OBJ_DISC) {
+    hit = ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p) && length(mk3(d[4], d[5], d[6]) - p) <= d[7] && t < h.t;
+  } else if (kind == FS_OBJ_QUAD_ONWH) {
+    if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p)) {
+      f3 ph = p - mk3(d[4], d[5], d[6]);
+      float td = dot(mk3(d[12], d[13], d[14]), ph);
+      float bd = dot(mk3(d[9], d[10], d[11]), ph);
+      hit = !(fabsf(bd) > d[7] || fabsf(td) > d[8]) && t < h.t;
+    }
+  } else if (kind == FS_OBJ_CUBOID) {
+    if (seg_box_cull(r, h.t, d + 24)) {
+      for (uint32_t i = 0; i < 6; i++) {
+        float ti;
+        if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, ti, p) && ti < h.t) {
+          bool ok = true;
+          for (uint32_t j = 0; j < 6; j++)
+            if (i / 2 != j / 2 && plane_dist(mk4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]), p) > 0.0f) ok = false;
+          if (ok) {
+            h.t = ti;
+            h.obj = (int32_t)oi;
+            h.prim = i;
+            hit = true;
+          }
+        }
+      }
+      if (hit) h.point = 0;
+      if (TEX && hit) h.tc = (int32_t)oi;
+      return hit;
+    }
+    return false;
+  }
+  if (hit) {
+    h.t = t;
+    h.obj = (int32_t)oi;
+    h.point = 0;
+    if (TEX) h.tc = (int32_t)oi;  // analytic objects always write texcoords
+  }
+  return hit;
+}
+
+// SceneBvhNode::Trace of leaf c (scene.cpp:76-103): the node test culls by
+// the best hit so far; the leaf traces its objects into ONE fresh
+// ObjectCollision (param 2, texcoords unset) and copies it whole into h each
+// time an object writes it with a param below h's.
+template <bool COUNT, bool TEX>
+__device__ bool scene_leaf_trace(const DevScene& S, uint32_t c, const Ray& r, bool zl, MinHit& h,
+                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally, const Slopes* slp) {
+  const DevSceneTree& T = *S.tree;
+  float np;
+  if (!ref_ray_bounds(mk3(T.child_mn[c][0], T.child_mn[c][1], T.child_mn[c][2]),
+                      mk3(T.child_mx[c][0], T.child_mx[c][1], T.child_mx[c][2]), r, zl, np) ||
+      np > h.t)
+    return false;
+  MinHit tmp;
+  tmp.t = 2.0f;
+  tmp.obj = -1;
+  tmp.prim = 0;
+  tmp.u = tmp.v = 0.0f;
+  tmp.point = 0;
+  tmp.tc = -1;
+  bool result = false;
+  const uint32_t first = T.first[c], cnt = T.count[c];
+  for (uint32_t k = 0; k < cnt; k++) {
+    if (object_trace<COUNT, TEX>(S, S.tree_objs[first + k], r, zl, tmp, stk, tally, slp) && tmp.t < h.t) {
+      h = tmp;
+      result = true;
+    }
+  }
+  return result;
+}
+
+// Scene::Trace through the object octree: SceneBvhNode::Trace of the root
+// (scene.cpp:76-84) and BaseBvhNode::TraceInternal (bvh.h:154-231) over its
+// eight leaves, with the reference's plane parameters and tie rules.
+template <bool COUNT, bool TEX>
+__device__ void scene_trace_tree(const DevScene& S, const Ray& r, MinHit& h, uint32_t* __restrict__ stk,
+                                 Tally<COUNT>& tally) {
+  h.t = 2.0f;
+  h.obj = -1;
+  h.prim = 0;
+  h.u = h.v = 0.0f;
+  h.point = 0;
+  h.tc = -1;
+  const bool zl = zero_len(r);
+  const Slopes sl = walk_slopes(r, zl);
+  const DevSceneTree& T = *S.tree;
+  const f3 rmn = mk3(T.root_mn[0], T.root_mn[1], T.root_mn[2]), rmx = mk3(T.root_mx[0], T.root_mx[1], T.root_mx[2]);
+  const f3 ctr = mk3(T.center[0], T.center[1], T.center[2]);
+  float rp;
+  f3 entry;
+  if (!ref_bounds_hit(rmn, rmx, r, zl, rp, entry)) return;  // (h.t = 2 never culls the root)
+  const f4 sx = mk4(T.split[0][0], T.split[0][1], T.split[0][2], T.split[0][3]);
+  const f4 sy = mk4(T.split[1][0], T.split[1][1], T.split[1][2], T.split[1][3]);
+  const f4 sz = mk4(T.split[2][0], T.split[2][1], T.split[2][2], T.split[2][3]);
+  float xp = 2.0f, yp = 2.0f, zp = 2.0f;  // collision() params of planes not hit
+  f3 xq = mk3(0, 0, 0), yq = xq, zq = xq;
+  bool xh, yh, zh;
+  uint32_t cn;
+  Ray it = r;
+  auto closest = [&](f3 q) {  // bvh.h:144-152: bit0 x, bit1 z, bit2 y
+    f3 dd = q - ctr;
+    return (uint32_t)(dd.x >= 0.0f) | ((uint32_t)(dd.z >= 0.0f) << 1) | ((uint32_t)(dd.y >= 0.0f) << 2);
+  };
+  if (!in_bounds(rmn, rmx, r.start)) {
+    it.start = entry;
+    cn = closest(entry);
+    xh = ray_plane(sx, it, xp, xq);
+    yh = ray_plane(sy, it, yp, yq);
+    zh = ray_plane(sz, it, zp, zq);
+  } else {
+    cn = closest(r.start);
+    xh = ray_plane(sx, r, xp, xq);
+    yh = ray_plane(sy, r, yp, yq);
+    zh = ray_plane(sz, r, zp, zq);
+    if (!xh && !yh && !zh) {
+      scene_leaf_trace<COUNT, TEX>(S, cn, r, zl, h, stk, tally, &sl);
+      return;
+    }
+  }
+  for (uint32_t i = 0; i < 4; i++) {
+    if (scene_leaf_trace<COUNT, TEX>(S, cn, r, zl, h, stk, tally, &sl)) {
+      const f3 hp = h.point ? r.start : r.start + r.dir * h.t;  // hit_info->point
+      if (in_bounds(mk3(T.child_mn[cn][0], T.child_mn[cn][1], T.child_mn[cn][2]),
+                    mk3(T.child_mx[cn][0], T.child_mx[cn][1], T.child_mx[cn][2]), hp))
+        break;
+    }
+    if (xh && xp < yp && xp < zp) {
+      cn ^= 1u;
+      xh = false;
+      it.start = xq;
+      xp = kInfinity;
+    } else if (yh && yp < zp && yp < xp) {
+      cn ^= 4u;
+      yh = false;
+      it.start = yq;
+      yp = kInfinity;
+    } else if (zh && zp < yp && zp < xp) {
+      cn ^= 2u;
+      zh = false;
+      it.start = zq;
+      zp = kInfinity;
+    } else {
+      break;
+    }
+    if (!in_bounds(rmn, rmx, it.start)) break;
+  }
+}
+
 // SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
 // resume it in a later call with the same ray: objects before the parked one
 // are skipped on resume (already processed), the rest follow in order.
-template <bool COUNT, bool TEX = false, bool SUSP = false>
+template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
                                                 bool* parked = nullptr) {
+  if (SOCT) {  // Scene::Trace with a valid object tree (scene.cpp:231-236)
+    scene_trace_tree<COUNT, TEX>(S, r, h, stk, tally);
+    return;
+  }
   bool resuming = SUSP && ws->oi >= 0;
   if (!resuming) {
     h.t = 2.0f;
@@ -1078,7 +1275,7 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 // keeps only (t, object, primitive, u, v); the per-bounce shading scalars
 // and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
 // AOVs go straight to the frame. Same outputs as render_kernel_regen.
-template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false>
+template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
@@ -1218,7 +1415,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
       const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
-      scene_trace_min<COUNT, TEX, SUSP>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
@@ -1247,7 +1444,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       }
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, TEX, SUSP>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
 #endif
       FS_PHASE(2);
       if (SUSP && parked) {
@@ -1414,6 +1611,7 @@ __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, cons
 
 // TraceRange (engine.cpp:298-329): one query per lane, the camera ray through
 // (x, y) without jitter or aperture, Scene::Trace, distance to the hit point.
+template <bool SOCT>
 __global__ __launch_bounds__(kBlock) void trace_range_kernel(DevScene S, DevCamera C, const float2* __restrict__ xy,
                                                              uint32_t n, float* __restrict__ out) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
@@ -1430,7 +1628,7 @@ __global__ __launch_bounds__(kBlock) void trace_range_kernel(DevScene S, DevCame
   MinHit h;
   Tally<false> tally;
   PhaseAcc pa;
-  scene_trace_min<false>(S, r, h, stk_all + threadIdx.x, tally, pa);
+  scene_trace_min<false, false, false, SOCT>(S, r, h, stk_all + threadIdx.x, tally, pa);
   float d = C.z_far;
   if (h.obj >= 0) {
     f3 p = h.point ? r.start : r.start + r.dir * h.t;
@@ -1547,7 +1745,7 @@ struct fs_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
   DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
-      pack_recv, range_io;
+      pack_recv, range_io, tree, tree_objs;
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= park_min_tris triangles: the PARKED schedule
@@ -1742,17 +1940,20 @@ struct LeanKernel {
   LeanFn fn;
   const char* name;
 };
-template <bool TEX, bool SUSP, bool MMAT>
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false>
 LeanKernel lean_kernel(bool count) {
   constexpr int W = SUSP ? FS_SUSP_WAVES : FS_LEAN_WAVES;
   static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
                                   (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
-                                  (MMAT ? "true" : "false") + ">";
-  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT>
-                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT>,
+                                  (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ">";
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT>,
           name.c_str()};
 }
-LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials) {
+// Scenes traced through the object octree take one instantiation that covers
+// textures and any material count (their object loop is per lane anyway).
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree) {
+  if (object_tree) return lean_kernel<true, false, true, true>(count);
   if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
   if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
   return many_materials ? lean_kernel<false, false, true>(count) : lean_kernel<false, false, false>(count);
@@ -1809,7 +2010,7 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order})
     b->release();
@@ -1891,6 +2092,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   if ((rc = upload(ctx, &ctx->tex_info, P.tex_info.data(), P.tex_info.size() * sizeof(uint32_t)))) return rc;
   if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
   if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
+  if ((rc = upload(ctx, &ctx->tree, &P.tree, P.tree_valid ? sizeof(DevSceneTree) : 0))) return rc;
+  if ((rc = upload(ctx, &ctx->tree_objs, P.tree_objs.data(), P.tree_objs.size() * sizeof(uint32_t)))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
   ctx->upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   ctx->gpu_bvh_ms = 0.0;
@@ -1930,6 +2133,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   S.tri_tex = (const float2*)ctx->tri_tex.p;
   S.tex_rgb = (const float*)ctx->tex_rgb.p;
   S.tex_info = (const uint4*)ctx->tex_info.p;
+  S.tree = P.tree_valid ? (const DevSceneTree*)ctx->tree.p : nullptr;
+  S.tree_objs = (const uint32_t*)ctx->tree_objs.p;
   S.num_objects = (uint32_t)P.objects.size();
   S.sky = P.sky;
   // Scene::SampleSky (scene.cpp:157-162): LightMaterial emissive x 3; a
@@ -2078,8 +2283,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // still walk. AUTO: PARKED when the scene has a mesh of >= park_min_tris
   // triangles and no texture (the textured instantiation has no parking).
   const bool parked = O.schedule == FS_SCHEDULE_PARKED ||
-                      (O.schedule == FS_SCHEDULE_AUTO && ctx->has_parking && !ctx->has_textures);
+                      (O.schedule == FS_SCHEDULE_AUTO && ctx->has_parking && !ctx->has_textures && !ctx->scene.tree);
   if (parked && ctx->has_textures) return fail(FS_ERR_INVALID, "the PARKED schedule does not take textured scenes");
+  if (parked && ctx->scene.tree)
+    return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
   // Sample groups: a launch renders G runs of `chunk` samples as
   // G x blocks blocks, then fold_groups folds them in order. G is sized so a
@@ -2127,9 +2334,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
   LeanRows rows;
-  const bool mm = ctx->many_materials;
-  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures, mm))) return rc;
-  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm);
+  const bool tree = ctx->scene.tree != nullptr;
+  const bool mm = ctx->many_materials || tree;
+  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures || tree, mm))) return rc;
+  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr);
   ctx->last_kernel = K.name;
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
@@ -2247,8 +2455,12 @@ int fs_trace_range(fs_context* ctx, const fs_camera* camera, uint32_t width, uin
   float* d_out = (float*)((char*)ctx->range_io.p + in_bytes);
   FS_HIP(hipMemcpyAsync(d_xy, xy, in_bytes, hipMemcpyHostToDevice, ctx->stream));
   DevCamera C = camera_basis(camera, width, height);
-  hipLaunchKernelGGL(dev::trace_range_kernel, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream,
-                     ctx->scene, C, d_xy, count, d_out);
+  if (ctx->scene.tree)
+    hipLaunchKernelGGL(dev::trace_range_kernel<true>, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       ctx->stream, ctx->scene, C, d_xy, count, d_out);
+  else
+    hipLaunchKernelGGL(dev::trace_range_kernel<false>, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       ctx->stream, ctx->scene, C, d_xy, count, d_out);
   FS_HIP(hipGetLastError());
   FS_HIP(hipMemcpyAsync(distances, d_out, 4ull * count, hipMemcpyDeviceToHost, ctx->stream));
   FS_HIP(hipStreamSynchronize(ctx->stream));

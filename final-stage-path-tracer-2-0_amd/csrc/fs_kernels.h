@@ -38,6 +38,8 @@ struct DevScene {
   const float* __restrict__ tex_rgb;   // all textures, 3 floats per texel
   const uint4* __restrict__ tex_info;  // first float, width, height, 0
   const float2* __restrict__ tri_tex;  // 3 texcoords per triangle (BVH order) or null
+  const DevSceneTree* __restrict__ tree;    // the object octree, or null (object-list walk)
+  const uint32_t* __restrict__ tree_objs;   // its leaves' object indices
   uint32_t num_objects;
   int32_t sky_tex;  // 1: the sky is a LightMaterial with a map
   int32_t sky;

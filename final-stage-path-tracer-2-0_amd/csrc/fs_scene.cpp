@@ -490,6 +490,200 @@ void put4(float* d, f4 v) {
 }
 
 // Builds one analytic object (object.cpp constructors).
+// The corners of a CuboidObject (object.cpp:115-124, volume.cpp:262-283),
+// rotated by cube::rotate about the box centre (volume.cpp:434-445).
+void cuboid_corners(const fs_object& o, f3 v[8]) {
+  const float* a = o.a;
+  f3 org = mk3(a[0], a[1], a[2]);
+  f3 half = mk3((float)(a[3] * 0.5), (float)(a[4] * 0.5), (float)(a[5] * 0.5));
+  Bounds bb;
+  bb.add(org - half);
+  bb.add(org + half);
+  f3 lo = bb.mn, hi = bb.mx;
+  const f3 box[8] = {lo,
+                     mk3(hi.x, lo.y, lo.z),
+                     mk3(hi.x, lo.y, hi.z),
+                     mk3(lo.x, lo.y, hi.z),
+                     mk3(lo.x, hi.y, lo.z),
+                     mk3(hi.x, hi.y, lo.z),
+                     mk3(hi.x, hi.y, hi.z),
+                     mk3(lo.x, hi.y, hi.z)};
+  for (int i = 0; i < 8; i++) v[i] = box[i];
+  if (o.rotate) {
+    f3 axis = mk3(a[6], a[7], a[8]);
+    float c = (float)std::cos(a[9]), s = (float)std::sin(a[9]);
+    f3 center = bb.center();
+    for (int i = 0; i < 8; i++) v[i] = rotate(v[i] - center, c, s, axis) + center;
+  }
+}
+
+// Object::GetBounds() as each constructor accumulates it: object.cpp:17-21
+// (sphere), 38-57 (plane: +-1000 along the in-plane axes), 75-95 (disc),
+// 115-124 + volume.cpp:434-445 (cuboid corners), 167-189 / 191-211 (quads),
+// mesh.cpp:218 (the transformed vertices). 2D objects get +-BASE_EPSILON
+// along their (raw) normal.
+Bounds object_bounds(const fs_object& o, const Bounds& mesh_rb) {
+  const float* a = o.a;
+  const f3 up = mk3(0, 1, 0);
+  const float eps = kEpsilon;
+  Bounds b;
+  switch (o.kind) {
+    case FS_OBJ_SPHERE: {
+      f3 org = mk3(a[0], a[1], a[2]), rr = mk3(a[3], a[3], a[3]);
+      b.add(org + rr);
+      b.add(org - rr);
+      break;
+    }
+    case FS_OBJ_PLANE: {
+      f3 n = mk3(a[0], a[1], a[2]);
+      float distance = -a[3];
+      f3 pop = n * distance;
+      f3 right = cross(n, up), forward = cross(n, right);
+      b.add(pop + right * 1000.0f);
+      b.add(pop - right * 1000.0f);
+      b.add(pop + forward * 1000.0f);
+      b.add(pop - forward * 1000.0f);
+      b.add(pop + n * eps);
+      b.add(pop - n * eps);
+      break;
+    }
+    case FS_OBJ_DISC: {
+      f3 org = mk3(a[0], a[1], a[2]), n = mk3(a[3], a[4], a[5]);
+      f3 right = cross(n, up), forward = cross(n, right);
+      b.add(org + right * a[6]);
+      b.add(org - right * a[6]);
+      b.add(org + forward * a[6]);
+      b.add(org - forward * a[6]);
+      b.add(org + n * eps);
+      b.add(org - n * eps);
+      break;
+    }
+    case FS_OBJ_CUBOID: {
+      f3 v[8];
+      cuboid_corners(o, v);
+      for (int i = 0; i < 8; i++) b.add(v[i]);
+      break;
+    }
+    case FS_OBJ_QUAD_ONWH: {
+      f3 n = mk3(a[3], a[4], a[5]), nrm = normalize(n), org = mk3(a[0], a[1], a[2]);
+      float hw = (float)(a[6] * 0.5), hh = (float)(a[7] * 0.5);
+      f3 bt = cross(nrm, up), tg = cross(nrm, bt);
+      b.add(org + bt * hw);
+      b.add(org - bt * hw);
+      b.add(org + tg * hh);
+      b.add(org - tg * hh);
+      b.add(org + n * eps);
+      b.add(org - n * eps);
+      break;
+    }
+    case FS_OBJ_QUAD_PUV: {
+      f3 pos = mk3(a[0], a[1], a[2]), u = mk3(a[3], a[4], a[5]), v = mk3(a[6], a[7], a[8]);
+      f3 nrm = normalize(cross(u, v));
+      f3 org = pos + u * (float)0.5 + v * (float)0.5;
+      float hw = (float)(length(u) * 0.5), hh = (float)(length(v) * 0.5);
+      f3 bt = normalize(u), tg = normalize(v);
+      b.add(org + nrm * eps);
+      b.add(org - nrm * eps);
+      b.add(org + bt * hw);
+      b.add(org - bt * hw);
+      b.add(org + tg * hh);
+      b.add(org - tg * hh);
+      break;
+    }
+    default:  // FS_OBJ_MESH
+      b = mesh_rb;
+      break;
+  }
+  return b;
+}
+
+// bounds::query_volume (volume.cpp:123-126) and bounds_intersect_bounds
+// (intersect.cpp:26-43) with BASE_PARAM_CHECK on (base.h:102): a box of zero
+// volume intersects nothing.
+float bounds_volume(const Bounds& b) { return (b.mx.x - b.mn.x) * (b.mx.y - b.mn.y) * (b.mx.z - b.mn.z); }
+bool bounds_overlap(const Bounds& a, const Bounds& b) {
+  if (0 == bounds_volume(a) || 0 == bounds_volume(b)) return false;
+  f3 ac = a.center(), bc = b.center();
+  f3 ae = a.mx - ac, be = b.mx - bc, dd = bc - ac;
+  return std::fabs(dd.x) <= (ae.x + be.x) && std::fabs(dd.y) <= (ae.y + be.y) && std::fabs(dd.z) <= (ae.z + be.z);
+}
+
+// SceneBvhNode::Subdivide's stop test (scene.cpp:37-46) for a node at `depth`
+// holding n objects, under max_tree_depth; min() is the Windows headers'
+// two-argument min (uint32 against double, a double result).
+bool scene_node_stops(uint32_t depth, uint32_t max_depth, size_t n) {
+  if (depth >= max_depth) return true;
+  const double a = (double)(uint32_t)(max_depth - depth);
+  const double b = (std::log((double)n) / std::log(8.0) + 0.5f) - 2.0f;
+  return (double)depth >= (a < b ? a : b);
+}
+
+// Scene::Optimize (scene.cpp:216-225) + SceneBvh::BuildBvh (:105-126) +
+// SceneBvhNode::Subdivide (:33-74) + ConfigureChildren (bvh.h:108-137).
+int build_scene_tree(const fs_scene_desc* d, const std::vector<Bounds>& ob, PreparedScene* S, std::string* err) {
+  const size_t n = d->num_objects;
+  const int32_t ideal = n ? (int32_t)((std::log((double)n) / std::log(8.0) + 0.5) - 2) : 0;
+  S->tree_valid = false;
+  if (!(d->flags & FS_SCENE_OPTIMIZED) || ideal <= 0) return FS_OK;
+  Bounds root;  // bounds += bounds (volume.cpp:193-224)
+  for (const Bounds& b : ob) {
+    if (root.count == 0) {
+      root.mn = b.mn;
+      root.mx = b.mx;
+      root.count = 1;
+      continue;
+    }
+    root.count++;
+    root.mx = mk3(b.mx.x > root.mx.x ? b.mx.x : root.mx.x, b.mx.y > root.mx.y ? b.mx.y : root.mx.y,
+                  b.mx.z > root.mx.z ? b.mx.z : root.mx.z);
+    root.mn = mk3(b.mn.x < root.mn.x ? b.mn.x : root.mn.x, b.mn.y < root.mn.y ? b.mn.y : root.mn.y,
+                  b.mn.z < root.mn.z ? b.mn.z : root.mn.z);
+  }
+  // The root node takes SceneBvhNode's default depth limit, 2 (scene.h:47,65).
+  constexpr uint32_t kRootMaxDepth = 2;
+  if (scene_node_stops(0, kRootMaxDepth, n) || n <= 2) {
+    *err = "scene object octree: the root would stay a leaf (unexpected for >= 182 objects)";
+    return FS_ERR_INVALID;
+  }
+  DevSceneTree& T = S->tree;
+  std::memset(&T, 0, sizeof(T));
+  put3(T.root_mn, root.mn);
+  put3(T.root_mx, root.mx);
+  const f3 mn = root.mn, center = root.center();
+  put3(T.center, center);
+  put4(T.split[0], plane_np(mk3(1, 0, 0), center));
+  put4(T.split[1], plane_np(mk3(0, 1, 0), center));
+  put4(T.split[2], plane_np(mk3(0, 0, 1), center));
+  const f3 hx = mk3(center.x, mn.y, mn.z) - mn, hy = mk3(mn.x, center.y, mn.z) - mn, hz = mk3(mn.x, mn.y, center.z) - mn;
+  const f3 span = hx + hy + hz;
+  Bounds child[8];
+  std::vector<std::vector<uint32_t>> lists(8);
+  for (int i = 0; i < 8; i++) {
+    f3 nmin = mn + hx * (float)(i % 2) + hy * (float)(i >> 2) + hz * (float)((i % 4) >> 1);
+    child[i].add(nmin);
+    child[i].add(nmin + span);
+    put3(T.child_mn[i], child[i].mn);
+    put3(T.child_mx[i], child[i].mx);
+  }
+  for (uint32_t j = 0; j < n; j++)
+    for (int i = 0; i < 8; i++)
+      if (bounds_overlap(ob[j], child[i])) lists[i].push_back(j);
+  S->tree_objs.clear();
+  for (int i = 0; i < 8; i++) {
+    // A child does not copy max_tree_depth_ (scene.cpp:20-25: undefined). With
+    // the parent's 2, or 0 or 1, Subdivide stops at depth 1 for any count.
+    if (!scene_node_stops(1, kRootMaxDepth, lists[i].size()) && lists[i].size() > 2) {
+      *err = "scene object octree: a leaf would subdivide (unexpected)";
+      return FS_ERR_INVALID;
+    }
+    T.first[i] = (uint32_t)S->tree_objs.size();
+    T.count[i] = (uint32_t)lists[i].size();
+    S->tree_objs.insert(S->tree_objs.end(), lists[i].begin(), lists[i].end());
+  }
+  S->tree_valid = true;
+  return FS_OK;
+}
+
 int build_object(const fs_object& o, DevObject* out, std::string* err) {
   std::memset(out, 0, sizeof(*out));
   out->kind = o.kind;
@@ -513,26 +707,8 @@ int build_object(const fs_object& o, DevObject* out, std::string* err) {
       return FS_OK;
     }
     case FS_OBJ_CUBOID: {  // object.cpp:115-124, volume.cpp:262-283, 434-445
-      f3 org = mk3(a[0], a[1], a[2]);
-      f3 half = mk3((float)(a[3] * 0.5), (float)(a[4] * 0.5), (float)(a[5] * 0.5));
-      Bounds bb;
-      bb.add(org - half);
-      bb.add(org + half);
-      f3 lo = bb.mn, hi = bb.mx;
-      f3 v[8] = {lo,
-                 mk3(hi.x, lo.y, lo.z),
-                 mk3(hi.x, lo.y, hi.z),
-                 mk3(lo.x, lo.y, hi.z),
-                 mk3(lo.x, hi.y, lo.z),
-                 mk3(hi.x, hi.y, lo.z),
-                 mk3(hi.x, hi.y, hi.z),
-                 mk3(lo.x, hi.y, hi.z)};
-      if (o.rotate) {
-        f3 axis = mk3(a[6], a[7], a[8]);
-        float c = (float)std::cos(a[9]), s = (float)std::sin(a[9]);
-        f3 center = bb.center();
-        for (int i = 0; i < 8; i++) v[i] = rotate(v[i] - center, c, s, axis) + center;
-      }
+      f3 v[8];
+      cuboid_corners(o, v);
       cube_planes(v, out->d);
       {  // padded corner box, same padding rule as the BVH node boxes
         f3 mn = v[0], mx = v[0];
@@ -885,6 +1061,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   // small meshes by lowering it).
   const uint32_t park_min = opt.park_min_tris;
   S.objects.resize(d->num_objects);
+  std::vector<Bounds> obj_bounds(d->num_objects);
   for (uint32_t i = 0; i < d->num_objects; i++) {
     const fs_object& o = d->objects[i];
     if (o.material < 0 || (uint32_t)o.material >= d->num_materials) {
@@ -909,11 +1086,14 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);
       put3(D.d + 3, mo.rb.mx);
+      obj_bounds[i] = mo.rb;
     } else {
       int rc = build_object(o, &S.objects[i], err);
       if (rc) return rc;
+      obj_bounds[i] = object_bounds(o, Bounds());
     }
   }
+  if (int rc = build_scene_tree(d, obj_bounds, &S, err)) return rc;
   S.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return FS_OK;
 }

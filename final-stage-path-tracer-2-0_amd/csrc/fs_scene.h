@@ -100,6 +100,20 @@ static_assert(sizeof(DevTri) == 80, "DevTri layout");
 inline uint32_t tri_face_host(const DevTri& t) { return t.face; }
 #endif
 
+// The reference's scene object octree (SceneBvh, scene.cpp:11-133), built
+// when Scene::Optimize ran and the scene has >= 182 objects (scene.cpp:216-
+// 225). Its root always splits into 8 leaves and no leaf splits again (the
+// root's depth limit is kMaxSubdivisionDepth = 2, scene.h:47, and
+// SceneBvhNode::Subdivide stops at depth 1 for any object count: DESIGN.md
+// §3b). Boxes and split planes are computed with the reference's float ops.
+struct DevSceneTree {
+  float root_mn[3], root_mx[3];
+  float center[3];                    // bounds::query_center of the root
+  float split[3][4];                  // split_planes_[0..2] (x, y, z)
+  float child_mn[8][3], child_mx[8][3];
+  uint32_t first[8], count[8];        // each leaf's object indices in tree_objs
+};
+
 // A mesh whose BVH is built on the device (fs_upload_scene_ex with
 // FS_UPLOAD_GPU_BVH, fs_bvh_gpu.hip). Its node block (num_tris nodes from
 // node_base) and triangle slots (num_tris from tri_base, plus normal and
@@ -129,6 +143,9 @@ struct PreparedScene {
   std::vector<DeferredMesh> deferred;  // meshes left for the device build
   uint32_t deferred_nodes = 0, deferred_tris = 0;  // device-only slots after the host arrays
   bool any_normals = false, any_tex = false;       // per-triangle normal / texcoord arrays exist
+  bool tree_valid = false;                         // the object octree is built (DevSceneTree)
+  DevSceneTree tree{};
+  std::vector<uint32_t> tree_objs;                 // leaf object lists, leaf after leaf
 };
 
 // The scene-build part of fs_options, validated (out-of-range values take

@@ -67,7 +67,10 @@ class fs_scene_desc(C.Structure):
                 ("sky_material", C.c_int32), ("objects", C.POINTER(fs_object)),
                 ("num_objects", C.c_uint32), ("meshes", C.POINTER(fs_mesh)),
                 ("num_meshes", C.c_uint32), ("textures", C.POINTER(fs_texture)),
-                ("num_textures", C.c_uint32), ("normal_table", C.POINTER(C.c_float))]
+                ("num_textures", C.c_uint32), ("normal_table", C.POINTER(C.c_float)), ("flags", C.c_uint32)]
+
+
+SCENE_OPTIMIZED = 1  # FS_SCENE_OPTIMIZED
 
 
 class fs_camera(C.Structure):

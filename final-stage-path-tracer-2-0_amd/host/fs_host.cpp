@@ -662,42 +662,50 @@ void Scene::SetSkyMaterial(std::shared_ptr<Material> material) {
 MeshObject* Scene::AddMeshObject(const std::string& filename, bool invert_normals, const vector3& translation,
                                  const vector3& scale, const vector4& rotation) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new MeshObject(filename, invert_normals, translation, scale, rotation));
   return static_cast<MeshObject*>(object_list_.back().get());
 }
 MeshObject* Scene::AddMeshObject(MeshData data, bool invert_normals, const vector3& translation,
                                  const vector3& scale, const vector4& rotation) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new MeshObject(std::move(data), invert_normals, translation, scale, rotation));
   return static_cast<MeshObject*>(object_list_.back().get());
 }
 SphericalObject* Scene::AddSphericalObject(const vector3& origin, float32 radius) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new SphericalObject(origin, radius));
   return static_cast<SphericalObject*>(object_list_.back().get());
 }
 DiscObject* Scene::AddDiscObject(const vector3& origin, const vector3& normal, float32 radius) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new DiscObject(origin, normal, radius));
   return static_cast<DiscObject*>(object_list_.back().get());
 }
 PlanarObject* Scene::AddPlanarObject(const plane& data) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new PlanarObject(data));
   return static_cast<PlanarObject*>(object_list_.back().get());
 }
 CuboidObject* Scene::AddCuboidObject(const vector3& origin, float32 width, float32 height, float32 depth) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new CuboidObject(origin, width, height, depth));
   return static_cast<CuboidObject*>(object_list_.back().get());
 }
 QuadObject* Scene::AddQuadObject(const vector3& origin, const vector3& normal, float32 width, float32 height) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new QuadObject(origin, normal, width, height));
   return static_cast<QuadObject*>(object_list_.back().get());
 }
 QuadObject* Scene::AddQuadObject(const vector3& position, const vector3& u, const vector3& v) {
   Touch();
+  optimized_ = false;  // is_tree_valid_ = false (scene.cpp:165-214)
   object_list_.emplace_back(new QuadObject(position, u, v));
   return static_cast<QuadObject*>(object_list_.back().get());
 }
@@ -909,6 +917,7 @@ const fs_scene_desc* Scene::Describe(std::string* err) {
   desc_.textures = desc_tex_.empty() ? nullptr : desc_tex_.data();
   desc_.num_textures = (uint32_t)desc_tex_.size();
   desc_.normal_table = g_normal_table.data();
+  desc_.flags = optimized_ ? FS_SCENE_OPTIMIZED : 0u;
   return &desc_;
 }
 

@@ -313,8 +313,15 @@ class Scene {
   void SetSkyMaterial(std::shared_ptr<LightMaterial> material);
   void SetSkyMaterial(std::shared_ptr<Material> material);  // scene.cpp:383 cast
   Material* GetSkyMaterial() { return sky_material_.get(); }
-  // Kept for API parity; the GPU path always uses per-mesh BVHs.
-  void Optimize() {}
+  // scene.cpp:216-225: marks the object list as optimised; the consumers
+  // (device layer, oracle) then trace a scene of >= 182 objects through the
+  // reference's object octree (fs_scene_desc.flags FS_SCENE_OPTIMIZED).
+  // Adding an object clears it, as in the reference.
+  void Optimize() {
+    optimized_ = true;
+    Touch();
+  }
+  bool optimized() const { return optimized_; }
   uint32 GetCameraCount() { return (uint32)camera_list_.size(); }
   Camera* GetCamera(uint32 index);
 
@@ -330,6 +337,7 @@ class Scene {
   std::vector<Camera> camera_list_;
   std::vector<std::unique_ptr<Object>> object_list_;
   uint64 version_ = 1;
+  bool optimized_ = false;  // Scene::is_tree_valid_ once Optimize() ran
   std::string last_error_;
   // Describe() storage
   std::vector<std::shared_ptr<Material>> desc_mat_ptrs_;

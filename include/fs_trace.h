@@ -142,7 +142,15 @@ typedef struct fs_scene_desc {
   uint32_t num_textures;
   /* normal_sphere table (normal.cpp:9-27), FS_NORMAL_TABLE_SIZE x 3 floats */
   const float* normal_table;
+  uint32_t flags;               /* FS_SCENE_* */
 } fs_scene_desc;
+
+/* Scene::Optimize() ran after the last object was added (LoadScene always
+ * calls it, scene.cpp:530; AddXObject clears it, scene.cpp:165-214). With it,
+ * a scene of >= 182 objects is traced through the reference's object octree
+ * (SceneBvh, scene.cpp:11-133, 216-236), as the reference does; without it,
+ * or with fewer objects, through the object list. */
+#define FS_SCENE_OPTIMIZED 1u
 
 /* Camera POD, camera.h:43-63. */
 typedef struct fs_camera {

@@ -660,6 +660,7 @@ typedef struct oobj {
   float hw, hh; v3 bitan, tan;      /* quad */
   v3 cverts[8]; v4 cplanes[6];      /* cuboid */
   int mesh;
+  bounds_t bb;                      /* Object::GetBounds() (object.cpp, mesh.cpp:218) */
 } oobj;
 
 /* ObjectCollision (object.h:47-61); surface_texcoords default to vector2()
@@ -668,6 +669,17 @@ typedef struct ocoll { float param; v3 point; v3 normal; int mat; int internal; 
 
 typedef struct otex { float* rgb; uint32_t w, h; } otex; /* Texture (material.h:42-52) */
 
+/* SceneBvhNode (scene.cpp:11-103): an object octree over the object list. */
+typedef struct snode {
+  bounds_t aabb;
+  uint32_t depth, max_depth;
+  int leaf;
+  v4 split[3];
+  int32_t child[8];
+  uint32_t* objs;
+  uint32_t nobjs, cap;
+} snode;
+
 struct oracle_scene {
   fs_material* mats; uint32_t nmats;
   int sky;
@@ -675,6 +687,8 @@ struct oracle_scene {
   omesh* meshes; uint32_t nmeshes;
   v3* table; uint32_t ntable;
   otex* texs; uint32_t ntex;
+  int tree_valid;                   /* Scene::is_tree_valid_ (scene.cpp:216-225) */
+  snode* snodes; uint32_t nsnodes, capsnodes;
 };
 
 /* planar_map_texcoords (intersect.cpp:769-778) */
@@ -804,6 +818,75 @@ static int build_object(oobj* o, const fs_object* d) {
   return 0;
 }
 
+/* Object::GetBounds() as each constructor accumulates it (object.cpp:17-21,
+ * 38-57, 75-95, 115-124 + volume.cpp:434-445, 167-211; mesh.cpp:218). Bounds
+ * are min/max accumulators, so only the points matter, not their order. */
+static void object_bounds(oobj* o, const fs_object* d, const oracle_scene* sc) {
+  const float* a = d->a;
+  bounds_t* b = &o->bb;
+  bounds_clear(b);
+  const v3 up = mk3(0, 1, 0);
+  const float eps = REF_EPSILON;
+  switch (d->kind) {
+    case FS_OBJ_SPHERE: {
+      v3 rr = mk3(o->radius, o->radius, o->radius);
+      bounds_add(b, add3(o->origin, rr));
+      bounds_add(b, sub3(o->origin, rr));
+      break;
+    }
+    case FS_OBJ_PLANE: {
+      v3 n = mk3(a[0], a[1], a[2]);
+      float distance = -a[3];
+      v3 pop = scl3(n, distance);
+      v3 right = cross3(n, up), forward = cross3(n, right);
+      bounds_add(b, add3(pop, scl3(right, 1000.0f)));
+      bounds_add(b, sub3(pop, scl3(right, 1000.0f)));
+      bounds_add(b, add3(pop, scl3(forward, 1000.0f)));
+      bounds_add(b, sub3(pop, scl3(forward, 1000.0f)));
+      bounds_add(b, add3(pop, scl3(n, eps)));
+      bounds_add(b, sub3(pop, scl3(n, eps)));
+      break;
+    }
+    case FS_OBJ_DISC: {
+      v3 n = mk3(a[3], a[4], a[5]);
+      v3 right = cross3(n, up), forward = cross3(n, right);
+      bounds_add(b, add3(o->origin, scl3(right, o->radius)));
+      bounds_add(b, sub3(o->origin, scl3(right, o->radius)));
+      bounds_add(b, add3(o->origin, scl3(forward, o->radius)));
+      bounds_add(b, sub3(o->origin, scl3(forward, o->radius)));
+      bounds_add(b, add3(o->origin, scl3(n, eps)));
+      bounds_add(b, sub3(o->origin, scl3(n, eps)));
+      break;
+    }
+    case FS_OBJ_CUBOID: /* cube::query_bounds(): the box, or its rotated corners (cube::rotate) */
+      for (int i = 0; i < 8; i++) bounds_add(b, o->cverts[i]);
+      break;
+    case FS_OBJ_QUAD_ONWH: {
+      v3 n = mk3(a[3], a[4], a[5]); /* the raw normal argument (object.cpp:187-188) */
+      bounds_add(b, add3(o->origin, scl3(o->bitan, o->hw)));
+      bounds_add(b, sub3(o->origin, scl3(o->bitan, o->hw)));
+      bounds_add(b, add3(o->origin, scl3(o->tan, o->hh)));
+      bounds_add(b, sub3(o->origin, scl3(o->tan, o->hh)));
+      bounds_add(b, add3(o->origin, scl3(n, eps)));
+      bounds_add(b, sub3(o->origin, scl3(n, eps)));
+      break;
+    }
+    case FS_OBJ_QUAD_PUV: {
+      v3 n = mk3(o->plane.x, o->plane.y, o->plane.z);
+      bounds_add(b, add3(o->origin, scl3(n, eps)));
+      bounds_add(b, sub3(o->origin, scl3(n, eps)));
+      bounds_add(b, add3(o->origin, scl3(o->bitan, o->hw)));
+      bounds_add(b, sub3(o->origin, scl3(o->bitan, o->hw)));
+      bounds_add(b, add3(o->origin, scl3(o->tan, o->hh)));
+      bounds_add(b, sub3(o->origin, scl3(o->tan, o->hh)));
+      break;
+    }
+    case FS_OBJ_MESH:
+      *b = sc->meshes[o->mesh].aabb;
+      break;
+  }
+}
+
 static inline void take(ocoll* h, const coll_t* c, int mat) {
   h->param = c->param; h->point = c->point; h->normal = c->normal; h->mat = mat;
   planar_map_tc(c->point, c->normal, &h->tu, &h->tv);  /* object.cpp:67-68, 106-107, 231-232 */
@@ -890,11 +973,187 @@ static int object_trace(const oracle_scene* sc, const oobj* o, const ray_t* r, o
   return 0;
 }
 
+/* ---- the scene object octree (scene.cpp:11-133, bvh.h:108-231) ---------- */
+static uint32_t new_snode(oracle_scene* sc) {
+  if (sc->nsnodes == sc->capsnodes) {
+    sc->capsnodes = sc->capsnodes ? 2 * sc->capsnodes : 16;
+    sc->snodes = (snode*)realloc(sc->snodes, sizeof(snode) * sc->capsnodes);
+  }
+  snode* n = &sc->snodes[sc->nsnodes];
+  memset(n, 0, sizeof(*n));
+  n->leaf = 1;
+  for (int i = 0; i < 8; i++) n->child[i] = -1;
+  return sc->nsnodes++;
+}
+static void snode_add(snode* n, uint32_t i) {
+  if (n->nobjs == n->cap) { n->cap = n->cap ? 2 * n->cap : 16; n->objs = (uint32_t*)realloc(n->objs, 4 * n->cap); }
+  n->objs[n->nobjs++] = i;
+}
+/* bounds::query_volume (volume.cpp:123-126) */
+static inline float bounds_volume(const bounds_t* b) {
+  return (b->mx.x - b->mn.x) * (b->mx.y - b->mn.y) * (b->mx.z - b->mn.z);
+}
+/* bounds_intersect_bounds (intersect.cpp:26-43), BASE_PARAM_CHECK on (base.h:102):
+ * a box of zero volume intersects nothing. */
+static int bounds_vs_bounds(const bounds_t* a, const bounds_t* b) {
+  if (0 == bounds_volume(a) || 0 == bounds_volume(b)) return 0;
+  v3 ac = bounds_center(a), bc = bounds_center(b);
+  v3 ae = sub3(a->mx, ac), be = sub3(b->mx, bc), d = sub3(bc, ac);
+  return fabsf(d.x) <= (ae.x + be.x) && fabsf(d.y) <= (ae.y + be.y) && fabsf(d.z) <= (ae.z + be.z);
+}
+/* bvh.h:108-137 on a scene node */
+static void sconfigure_children(oracle_scene* sc, uint32_t ni) {
+  v3 mn = sc->snodes[ni].aabb.mn;
+  v3 center = bounds_center(&sc->snodes[ni].aabb);
+  v3 hx = sub3(mk3(center.x, mn.y, mn.z), mn);
+  v3 hy = sub3(mk3(mn.x, center.y, mn.z), mn);
+  v3 hz = sub3(mk3(mn.x, mn.y, center.z), mn);
+  v3 span = add3(add3(hx, hy), hz);
+  sc->snodes[ni].split[0] = plane_np(mk3(1, 0, 0), center);
+  sc->snodes[ni].split[1] = plane_np(mk3(0, 1, 0), center);
+  sc->snodes[ni].split[2] = plane_np(mk3(0, 0, 1), center);
+  for (int i = 0; i < 8; i++) {
+    uint32_t c = new_snode(sc); /* may realloc */
+    snode* parent = &sc->snodes[ni];
+    /* SceneBvhNode(parent) copies neither max_tree_depth_ nor anything but
+     * depth/parent/objects (scene.cpp:20-25): the member is left
+     * uninitialised, undefined behaviour. Convention here: the child inherits
+     * its parent's value (0 or 1 give the same tree: see DESIGN.md §3b). */
+    sc->snodes[c].depth = parent->depth + 1;
+    sc->snodes[c].max_depth = parent->max_depth;
+    parent->child[i] = (int32_t)c;
+    v3 nmin = add3(add3(add3(mn, scl3(hx, (float)(i % 2))), scl3(hy, (float)(i >> 2))), scl3(hz, (float)((i % 4) >> 1)));
+    v3 nmax = add3(nmin, span);
+    bounds_t nb; bounds_clear(&nb);
+    bounds_add(&nb, nmin);
+    bounds_add(&nb, nmax);
+    sc->snodes[c].aabb = nb;
+  }
+  sc->snodes[ni].leaf = 0;
+}
+/* SceneBvhNode::Subdivide (scene.cpp:33-74). min() is the two-argument min of
+ * the Windows headers: uint32 against double compares and yields a double. */
+static void ssubdivide(oracle_scene* sc, uint32_t ni) {
+  snode* n = &sc->snodes[ni];
+  if (n->depth >= n->max_depth) return;
+  double a = (double)(uint32_t)(n->max_depth - n->depth);
+  double b = (log((double)n->nobjs) / log(8.0) + 0.5f) - 2.0f;
+  double mn = a < b ? a : b;
+  if ((double)n->depth >= mn) return;
+  if (n->nobjs > 2) { /* kMaxObjectCountPerNode (scene.cpp:9) */
+    sconfigure_children(sc, ni);
+    n = &sc->snodes[ni];
+    for (uint32_t j = 0; j < n->nobjs; j++) {
+      uint32_t oi = n->objs[j];
+      for (int i = 0; i < 8; i++) {
+        snode* c = &sc->snodes[sc->snodes[ni].child[i]];
+        if (bounds_vs_bounds(&sc->objs[oi].bb, &c->aabb)) snode_add(c, oi);
+      }
+    }
+    free(sc->snodes[ni].objs);
+    sc->snodes[ni].objs = NULL;
+    sc->snodes[ni].nobjs = sc->snodes[ni].cap = 0;
+    for (int j = 0; j < 8; j++) ssubdivide(sc, (uint32_t)sc->snodes[ni].child[j]);
+  }
+}
+/* Scene::Optimize (scene.cpp:216-225) + SceneBvh::BuildBvh (:105-126). */
+static void scene_optimize(oracle_scene* sc) {
+  sc->tree_valid = 0;
+  int32_t ideal = (int32_t)((log((double)sc->nobjs) / log(8.0) + 0.5) - 2);
+  if (!sc->nobjs || ideal <= 0) return;
+  uint32_t root = new_snode(sc);
+  sc->snodes[root].max_depth = 2; /* SceneBvhNode(data_source) default, kMaxSubdivisionDepth (scene.h:47) */
+  bounds_t rb; bounds_clear(&rb);
+  for (uint32_t i = 0; i < sc->nobjs; i++) { /* bounds += bounds (volume.cpp:193-224) */
+    const bounds_t* ob = &sc->objs[i].bb;
+    if (rb.count == 0) { rb.mn = ob->mn; rb.mx = ob->mx; rb.count = 1; continue; }
+    rb.count++;
+    if (ob->mx.x > rb.mx.x) rb.mx.x = ob->mx.x;
+    if (ob->mx.y > rb.mx.y) rb.mx.y = ob->mx.y;
+    if (ob->mx.z > rb.mx.z) rb.mx.z = ob->mx.z;
+    if (ob->mn.x < rb.mn.x) rb.mn.x = ob->mn.x;
+    if (ob->mn.y < rb.mn.y) rb.mn.y = ob->mn.y;
+    if (ob->mn.z < rb.mn.z) rb.mn.z = ob->mn.z;
+  }
+  sc->snodes[root].aabb = rb;
+  for (uint32_t i = 0; i < sc->nobjs; i++) snode_add(&sc->snodes[root], i);
+  ssubdivide(sc, root);
+  sc->tree_valid = 1;
+}
+
+static int snode_trace(const oracle_scene* sc, uint32_t ni, const ray_t* r, ocoll* h, tstats* st);
+/* bvh.h:154-231 with SceneBvhNode children */
+static int strace_internal(const oracle_scene* sc, uint32_t ni, coll_t node_hit, const ray_t* r, ocoll* h,
+                           tstats* st) {
+  const snode* n = &sc->snodes[ni];
+  int result = 0, xh, yh, zh;
+  uint32_t cn;
+  ray_t it = *r;
+  coll_t xi = no_coll(), yi = no_coll(), zi = no_coll();
+  if (!point_in_bounds(&n->aabb, r->start)) {
+    it.start = node_hit.point;
+    v3 d = sub3(node_hit.point, bounds_center(&n->aabb));
+    cn = ((d.x >= 0.0f) | ((d.z >= 0.0f) << 1) | ((d.y >= 0.0f) << 2)) & 0xFF;
+    xh = ray_plane(n->split[0], &it, &xi);
+    yh = ray_plane(n->split[1], &it, &yi);
+    zh = ray_plane(n->split[2], &it, &zi);
+  } else {
+    v3 d = sub3(r->start, bounds_center(&n->aabb));
+    cn = ((d.x >= 0.0f) | ((d.z >= 0.0f) << 1) | ((d.y >= 0.0f) << 2)) & 0xFF;
+    xh = ray_plane(n->split[0], r, &xi);
+    yh = ray_plane(n->split[1], r, &yi);
+    zh = ray_plane(n->split[2], r, &zi);
+    if (!xh && !yh && !zh) return snode_trace(sc, (uint32_t)n->child[cn], r, h, st);
+  }
+  for (uint32_t i = 0; i < 4; i++) {
+    if (snode_trace(sc, (uint32_t)n->child[cn], r, h, st)) {
+      result = 1;
+      if (point_in_bounds(&sc->snodes[n->child[cn]].aabb, h->point)) break;
+    }
+    if (xh && xi.param < yi.param && xi.param < zi.param) {
+      cn ^= 0x1; xh = 0; it.start = xi.point; xi.param = REF_INFINITY;
+    } else if (yh && yi.param < zi.param && yi.param < xi.param) {
+      cn ^= 0x4; yh = 0; it.start = yi.point; yi.param = REF_INFINITY;
+    } else if (zh && zi.param < yi.param && zi.param < xi.param) {
+      cn ^= 0x2; zh = 0; it.start = zi.point; zi.param = REF_INFINITY;
+    } else {
+      break;
+    }
+    if (!point_in_bounds(&n->aabb, it.start)) break;
+  }
+  return result;
+}
+/* SceneBvhNode::Trace (scene.cpp:76-103): a leaf traces its objects into ONE
+ * fresh ObjectCollision (param 2, texcoords (0,0)) and copies it whole into
+ * hit_info each time it beats hit_info's param. */
+static int snode_trace(const oracle_scene* sc, uint32_t ni, const ray_t* r, ocoll* h, tstats* st) {
+  const snode* n = &sc->snodes[ni];
+  coll_t nh = no_coll();
+  if (!ray_bounds(&n->aabb, r, &nh) || nh.param > h->param) return 0;
+  if (!n->leaf) return strace_internal(sc, ni, nh, r, h, st);
+  int result = 0;
+  ocoll temp;
+  temp.param = 2.0f; temp.point = mk3(0, 0, 0); temp.normal = mk3(0, 0, 0); temp.mat = -1; temp.internal = 0;
+  temp.tu = temp.tv = 0.0f;
+  for (uint32_t i = 0; i < n->nobjs; i++) {
+    if (object_trace(sc, &sc->objs[n->objs[i]], r, &temp, st)) {
+      if (temp.param < h->param) {
+        *h = temp;
+        result = 1;
+      }
+    }
+  }
+  return result;
+}
+
 static int scene_trace(const oracle_scene* sc, const ray_t* r, ocoll* h, tstats* st) {
   int det = 0;
   h->param = 2.0f; h->point = mk3(0, 0, 0); h->normal = mk3(0, 0, 0); h->mat = -1; h->internal = 0;
   h->tu = h->tv = 0.0f;
-  for (uint32_t i = 0; i < sc->nobjs; i++) det |= object_trace(sc, &sc->objs[i], r, h, st);
+  if (sc->tree_valid)
+    det = snode_trace(sc, 0, r, h, st); /* SceneBvh::Trace (scene.cpp:128-133) */
+  else
+    for (uint32_t i = 0; i < sc->nobjs; i++) det |= object_trace(sc, &sc->objs[i], r, h, st);
   v4 cp = plane_np(h->normal, h->point);
   if (plane_dist(cp, r->start) < 0.0) {
     h->normal = scl3(h->normal, (float)-1.0);
@@ -1195,7 +1454,9 @@ int oracle_scene_create(const fs_scene_desc* d, oracle_scene** out) {
     if (o->material < 0 || (uint32_t)o->material >= s->nmats) rc = FS_ERR_INVALID;
     else if (o->kind == FS_OBJ_MESH && (o->mesh < 0 || (uint32_t)o->mesh >= s->nmeshes)) rc = FS_ERR_INVALID;
     else rc = build_object(&s->objs[i], o);
+    if (!rc) object_bounds(&s->objs[i], o, s);
   }
+  if (!rc && (d->flags & FS_SCENE_OPTIMIZED)) scene_optimize(s);
   if (rc) { oracle_scene_destroy(s); return rc; }
   *out = s;
   return 0;
@@ -1205,6 +1466,8 @@ void oracle_scene_destroy(oracle_scene* s) {
   if (!s) return;
   for (uint32_t i = 0; i < s->nmeshes; i++) mesh_free(&s->meshes[i]);
   for (uint32_t i = 0; i < s->ntex; i++) free(s->texs[i].rgb);
+  for (uint32_t i = 0; i < s->nsnodes; i++) free(s->snodes[i].objs);
+  free(s->snodes);
   free(s->texs); free(s->meshes); free(s->objs); free(s->mats); free(s->table); free(s);
 }
 
@@ -1471,4 +1734,20 @@ int oracle_face_leaves(const oracle_scene* sc, uint32_t mesh, uint32_t f, uint32
       }
   }
   return (int)n;
+}
+
+/* The scene object octree (tests/tools): node i's box, leaf flag, children
+ * and object list (up to max). Returns the node count (0: no tree). */
+int oracle_scene_tree(const oracle_scene* sc, uint32_t i, float* box, int32_t* children, uint32_t* count,
+                      uint32_t* objs, uint32_t max) {
+  if (!sc->tree_valid) return 0;
+  if (i < sc->nsnodes) {
+    const snode* n = &sc->snodes[i];
+    box[0] = n->aabb.mn.x; box[1] = n->aabb.mn.y; box[2] = n->aabb.mn.z;
+    box[3] = n->aabb.mx.x; box[4] = n->aabb.mx.y; box[5] = n->aabb.mx.z;
+    for (int k = 0; k < 8; k++) children[k] = n->leaf ? -1 : n->child[k];
+    *count = n->nobjs;
+    for (uint32_t k = 0; k < n->nobjs && k < max; k++) objs[k] = n->objs[k];
+  }
+  return (int)sc->nsnodes;
 }

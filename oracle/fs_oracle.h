@@ -90,6 +90,11 @@ int oracle_object_trace(const oracle_scene* scene, uint32_t obj, const float sta
 int oracle_face_leaves(const oracle_scene* scene, uint32_t mesh, uint32_t f, uint32_t* leaves, float* boxes,
                        uint32_t max);
 
+/* The scene object octree (SceneBvh): node i's box (min, max), its 8
+ * children (-1 for a leaf), its object count and up to max object indices.
+ * Returns the number of nodes, 0 when the scene is traced through its list. */
+int oracle_scene_tree(const oracle_scene* scene, uint32_t i, float box[6], int32_t children[8], uint32_t* count,
+                      uint32_t* objs, uint32_t max);
 /* Logs the octree walk's decisions to stderr while on (not thread-safe). */
 void oracle_set_walk_log(int on);
 

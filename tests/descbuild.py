@@ -87,7 +87,9 @@ class DescBuilder:
         self.meshes.append(m)
         return self.obj(fsamd.OBJ_MESH, mat, [], mesh=len(self.meshes) - 1)
 
-    def build(self):
+    def build(self, optimized=False):
+        """optimized: Scene::Optimize() ran (FS_SCENE_OPTIMIZED): scenes of
+        >= 182 objects are traced through the object octree."""
         fsamd.initialize_materials()
         self.table = fsamd.normal_table()
         d = fsamd.fs_scene_desc()
@@ -106,6 +108,7 @@ class DescBuilder:
             d.textures = C.cast(self._texs, C.POINTER(fsamd.fs_texture))
             d.num_textures = len(self.textures)
         d.normal_table = self.table.ctypes.data_as(C.POINTER(C.c_float))
+        d.flags = fsamd.SCENE_OPTIMIZED if optimized else 0
         self.desc = d
         return C.cast(C.pointer(d), C.c_void_p)
 

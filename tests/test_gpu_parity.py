@@ -682,7 +682,107 @@ def test_many_materials_bit_exact(variant, gpu_renderer):
         gpu_renderer.set_options(schedule="parked", park_min_tris=1)
     out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
     k = gpu_renderer.last_kernel()
-    assert k.endswith(", true>"), k  # the MMAT instantiation
+    assert k[:-1].split(", ")[4] == "true", k  # the MMAT instantiation <.., TEX, SUSP, MMAT, SOCT>
     assert (k[:-1].split(", ")[3] == "true") == (variant == "parked"), k
     ref = oracle_render(ptr, CAM, 96, 72, 16)
     assert_parity(out, ref, exact=True)
+
+
+# ---- the scene object octree (>= 182 objects, Scene::Optimize) -----------
+def crowd_scene(n_extra=200, textured=True):
+    """A Cornell room plus n_extra small objects of every kind (spheres,
+    cuboids, discs, both quad constructors), an infinite plane below the
+    room (its +-1000 bounds widen the octree root) and a back quad at
+    z = 500, whose +-BASE_EPSILON thickness rounds away: zero volume, so the
+    octree never lists it (intersect.cpp:28-32). Textured meshes and objects
+    exercise the leaf-local ObjectCollision texcoords (scene.cpp:87-96)."""
+    b = DescBuilder()
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(15, 15, 15))
+    cornell_room(b, white, red, light)
+    tex = b.texture(np.random.default_rng(9).random((16, 16, 3), dtype=np.float32)) if textured else -1
+    mapped = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.9, 0.9, 0.9), texture=tex, texture_scale=2.0)
+    metal = b.material(fsamd.MAT_METAL, diffuse=(0.9, 0.8, 0.6), roughness=0.3)
+    ceramic = b.material(fsamd.MAT_CERAMIC, diffuse=(0.3, 0.6, 0.9), shininess=0.6)
+    glass = b.material(fsamd.MAT_GLASS, diffuse=(0.95, 0.95, 0.95), index=0.67, reflectivity=0.1)
+    mats = [white, mapped, metal, ceramic, glass, red]
+    rng = np.random.default_rng(21)
+    for j in range(n_extra):
+        m = mats[j % len(mats)]
+        x, y, z = (float(v) for v in rng.uniform([-9, 0.5, -9], [9, 19, 9]))
+        k = j % 5
+        if k == 0:
+            b.obj(fsamd.OBJ_SPHERE, m, [x, y, z, float(rng.uniform(0.2, 0.9))])
+        elif k == 1:
+            b.obj(fsamd.OBJ_CUBOID, m, [x, y, z, 0.8, 0.6, 1.0, 0.2, 1.0, 0.4, float(rng.uniform(0, 3))], rotate=1)
+        elif k == 2:
+            b.obj(fsamd.OBJ_DISC, m, [x, y, z, 0.3, 0.2, -1.0, 0.7])
+        elif k == 3:
+            b.obj(fsamd.OBJ_QUAD_ONWH, m, [x, y, z, -0.2, 0.1, -1.0, 1.2, 0.9])
+        else:
+            b.obj(fsamd.OBJ_QUAD_PUV, m, [x, y, z, 1.0, 0.1, 0.0, 0.0, 0.9, 0.3])
+    # axis-aligned flat meshes (the room's side walls and ceiling light) have
+    # zero volume too, so the octree drops them: light comes from lamps
+    for x, z in ((-5, -5), (5, 5), (-5, 5), (5, -5)):
+        b.obj(fsamd.OBJ_SPHERE, light, [float(x), 18.5, float(z), 1.2])
+    b.obj(fsamd.OBJ_PLANE, white, [0.0, 1.0, 0.0, 5.0])  # y = -5, below the floor
+    b.obj(fsamd.OBJ_QUAD_ONWH, red, [0.0, 10.0, 500.0, 0.0, 0.0, -1.0, 4000.0, 4000.0])
+    tc = np.float32([[0, 0], [1, 0], [1, 1], [0, 1]])
+    b.mesh(mapped, [[-4, 2, 3], [4, 2, 3], [4, 8, 3], [-4, 8, 3]], [[0, 1, 2], [0, 2, 3]], texcoords=tc,
+           corner_tex=[[0, 1, 2], [0, 2, 3]])
+    b.mesh(metal, [[-6, 12, 6], [2, 12, 6], [2, 16, 6]], [[0, 1, 2]])  # no texcoords: keeps stale ones
+    return b
+
+
+@pytest.mark.parametrize("optimized", [True, False])
+def test_object_octree_scene_bit_exact(optimized, gpu_renderer):
+    """A 212-object scene. Optimized, the reference traces it through its
+    object octree (scene.cpp:216-236): eight leaves under the root, leaf-local
+    collision records, the exit-parameter root cull, objects of zero volume
+    left out (the flat side walls, ceiling light and back quad disappear);
+    the GPU walks the same tree. Without Optimize, both walk the object
+    list. Bit-exact with the oracle either way, and the two modes render
+    different frames."""
+    b = crowd_scene()
+    ptr = b.build(optimized=optimized)
+    cam = fsamd.camera((0, 10, -34), (0, 10, 0), fov_y=40, aperture=0.0)
+    out = gpu_render(gpu_renderer, ptr, cam, 96, 72, 16)
+    k = gpu_renderer.last_kernel()
+    assert (k[:-1].split(", ")[-1] == "true") == optimized, k  # the object-octree instantiation
+    ref = oracle_render(ptr, cam, 96, 72, 16)
+    assert_parity(out, ref, exact=True)
+    _record("object_octree", {"optimized": optimized, "mean": float(out[fsamd.PLANE_COLOR].mean())})
+    other = oracle_render(crowd_scene().build(optimized=not optimized), cam, 96, 72, 16)
+    assert not np.array_equal(other.color, ref.color)
+
+
+def test_object_octree_loaded_scene_and_trace_range(tmp_path, gpu_renderer):
+    """A .scene file of 190 spheres through Scene::LoadScene (which always
+    calls Optimize, scene.cpp:530): GPU frame and TraceRange against the
+    oracle."""
+    lines = ["camera\n{\n  position 0 10 -34\n  target 0 10 0\n  fov 40\n  aperture 0\n}\n",
+             "material white\n{\n  color 0.73 0.73 0.73\n}\n",
+             "material lamp\n{\n  emission 12 12 12\n}\n",
+             "material glaze\n{\n  color 0.3 0.6 0.9\n  roughness 0.6\n}\n"]
+    rng = np.random.default_rng(4)
+    for j in range(190):
+        x, y, z = rng.uniform([-9, 0.5, -9], [9, 19, 9])
+        mat = ("white", "glaze", "lamp")[j % 3 if j % 17 else 2]
+        lines.append(f"sphere\n{{\n  material {mat}\n  position {x:.4f} {y:.4f} {z:.4f}\n"
+                     f"  radius {rng.uniform(0.3, 1.2):.3f}\n}}\n")
+    path = tmp_path / "crowd.scene"
+    path.write_text("".join(lines))
+    fsamd.reset_main_rng()
+    s = fsamd.HostScene.load(str(path))
+    fsamd.initialize_materials()
+    assert s.desc().contents.flags & fsamd.SCENE_OPTIMIZED and s.desc().contents.num_objects == 190
+    cam = s.camera(0)
+    out = gpu_render(gpu_renderer, s, cam, 80, 60, 8)
+    assert gpu_renderer.last_kernel()[:-1].split(", ")[-1] == "true"
+    ref = oracle_render(s.desc_ptr(), cam, 80, 60, 8)
+    assert_parity(out, ref, exact=True)
+    pts = np.random.default_rng(1).uniform([0, 0], [80, 60], (200, 2)).astype(np.float32)
+    o = oracle_py.Scene(s.desc_ptr())
+    np.testing.assert_array_equal(gpu_renderer.trace_range(cam, 80, 60, pts), o.trace_range(cam, 80, 60, pts))
+    o.close()
