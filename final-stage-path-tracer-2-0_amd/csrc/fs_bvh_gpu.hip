@@ -58,8 +58,7 @@ struct TaskData {
   uint32_t clo[2][3], chi[2][3];             // child boxes
   int32_t axis;                              // SAH split axis; -1: even split, -2: object median
   uint32_t bin, nl;                          // split bin, left count
-  uint32_t maxis, pivot, nless, ties;        // median: axis, pivot key, keys below it, ties taken
-  uint32_t fill[2];                          // partition cursors
+  uint32_t maxis, pivot, nless;              // median: axis, pivot key, keys below it
   int32_t child_task[2];                     // next-level task of each side, -1: none
 };
 
@@ -121,6 +120,14 @@ struct Build {
                        // [5] nodes built
   Task* small;         // phase-B subtrees (node = reserved block base)
   uint32_t max_nodes;
+  // Deterministic partition and numbering (the same tree, layout and
+  // triangle order on every run): per position, the exclusive prefix of
+  // (median ties << 32 | left positions), scanned per block of 256 and then
+  // over the blocks; per task, the exclusive prefix of its children's
+  // (next-level tasks, phase-B subtrees, nodes).
+  uint64_t* pre;        // per position
+  uint64_t* bsum;       // per block of 256 positions
+  uint4* plan;          // per task: next tasks, small subtrees, nodes, -
 };
 
 __device__ __forceinline__ float cen(const Build& B, uint32_t p, int k) {
@@ -350,36 +357,106 @@ __global__ __launch_bounds__(256) void k_select(Build B) {
   if (threadIdx.x == 0) {
     d.pivot = prefix;
     d.nless = (T.e - T.b) / 2 - rank;  // keys below the pivot
-    d.ties = 0;
   }
 }
 
-// Scatter of each position to its side of its task's range. Lanes of the
-// wave's lead task take their slots with one atomic per side per wave (ballot
-// prefix counts inside the wave) and reduce the child boxes across the wave.
+// The side of position p (task t, primitive q) in its task's split: 0 left,
+// 1 right; *tie for a median-split key equal to the pivot (its side is
+// decided by its rank among the task's ties, k_partition).
+__device__ __forceinline__ uint32_t side_of(const Build& B, uint32_t p, int32_t t, uint32_t q, bool* tie) {
+  const Task T = B.tasks[t];
+  const TaskData& d = B.td[t];
+  *tie = false;
+  if (d.axis == -2) {  // the n/2 smallest centroids on maxis go left
+    const uint32_t key = f2o(cen(B, q, (int)d.maxis));
+    if (key == d.pivot) {
+      *tie = true;
+      return 0u;
+    }
+    return key < d.pivot ? 0u : 1u;
+  }
+  if (d.axis < 0) return (p - T.b) < d.nl ? 0u : 1u;
+  const float cmin = o2f(d.cmin[d.axis]), ext = o2f(d.cmax[d.axis]) - cmin;
+  return (uint32_t)bin_of(cen(B, q, d.axis), cmin, ext) < d.bin ? 0u : 1u;
+}
+
+// Per position: (tie << 32) | (non-tie left), scanned exclusively within
+// each block of 256; the block totals go to bsum.
+__global__ __launch_bounds__(256) void k_prefix_local(Build B) {
+  __shared__ uint64_t wsum[4];
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t t = task_at(B, p);
+  uint64_t v = 0;
+  if (t >= 0) {
+    bool tie;
+    const uint32_t side = side_of(B, p, t, B.perm[p], &tie);
+    v = tie ? (1ull << 32) : (side == 0 ? 1ull : 0ull);
+  }
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint64_t x = v;  // inclusive wave scan (the two 32-bit halves never carry)
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint64_t off = 0;
+  for (uint32_t k = 0; k < w; k++) off += wsum[k];
+  if (p < B.n) B.pre[p] = off + x - v;
+  if (threadIdx.x == 255) B.bsum[blockIdx.x] = off + x;
+}
+
+// Exclusive scan of `count` 64-bit values in place, one block.
+__global__ __launch_bounds__(1024) void k_scan_block(uint64_t* v, uint32_t count) {
+  __shared__ uint64_t part[1024];
+  const uint32_t per = (count + 1023) / 1024, b = threadIdx.x * per, e = min(count, b + per);
+  uint64_t s = 0;
+  for (uint32_t i = b; i < e; i++) s += v[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele over the 1024 partial sums
+    const uint64_t y = threadIdx.x >= o ? part[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0ull;
+  for (uint32_t i = b; i < e; i++) {
+    const uint64_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+}
+
+__device__ __forceinline__ uint64_t prefix_at(const Build& B, uint32_t p) { return B.pre[p] + B.bsum[p >> 8]; }
+
+// Stable scatter of each position to its side of its task's range: a
+// position's slot is its rank among the task's positions of that side (the
+// scanned prefixes), and the median's ties go left in position order until
+// the left side holds n/2. The same input order gives the same output order
+// on every run. Lanes of the wave's lead task reduce the child boxes across
+// the wave.
 __global__ __launch_bounds__(256) void k_partition(Build B) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t t = task_at(B, p);
   const int32_t lead = __shfl(t, 0, 64);
-  const uint32_t lane = threadIdx.x & 63u;
   if (p < B.n && t < 0) B.perm2[p] = B.perm[p];
   uint32_t side = 0, q = 0;
   if (t >= 0) {
     const Task T = B.tasks[t];
     const TaskData& d = B.td[t];
     q = B.perm[p];
-    if (d.axis == -2) {  // the n/2 smallest centroids on maxis go left
-      const uint32_t key = f2o(cen(B, q, (int)d.maxis));
-      if (key != d.pivot)
-        side = key < d.pivot ? 0u : 1u;
-      else
-        side = atomicAdd(&B.td[t].ties, 1u) < d.nl - d.nless ? 0u : 1u;
-    } else if (d.axis < 0) {
-      side = (p - T.b) < d.nl ? 0u : 1u;
-    } else {
-      const float cmin = o2f(d.cmin[d.axis]), ext = o2f(d.cmax[d.axis]) - cmin;
-      side = (uint32_t)bin_of(cen(B, q, d.axis), cmin, ext) < d.bin ? 0u : 1u;
-    }
+    bool tie;
+    side = side_of(B, p, t, q, &tie);
+    const uint64_t a = prefix_at(B, p), a0 = prefix_at(B, T.b);
+    const uint32_t ties_before = (uint32_t)(a >> 32) - (uint32_t)(a0 >> 32);
+    const uint32_t lefts_before = (uint32_t)a - (uint32_t)a0;
+    const uint32_t quota = d.axis == -2 ? d.nl - d.nless : 0u;  // ties that go left
+    if (tie) side = ties_before < quota ? 0u : 1u;
+    const uint32_t left_rank = lefts_before + min(ties_before, quota);
+    const uint32_t np = side ? T.b + d.nl + (p - T.b - left_rank) : T.b + left_rank;
+    B.perm2[np] = q;
+    B.tag[np] = ((uint32_t)t << 1) | side;
   }
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   if (t >= 0)
@@ -389,10 +466,6 @@ __global__ __launch_bounds__(256) void k_partition(Build B) {
     }
   if (t >= 0 && t != lead) {
     TaskData& d = B.td[t];
-    const Task T = B.tasks[t];
-    const uint32_t np = T.b + (side ? d.nl : 0u) + atomicAdd(&d.fill[side], 1u);
-    B.perm2[np] = q;
-    B.tag[np] = ((uint32_t)t << 1) | side;
     for (int c = 0; c < 3; c++) {
       atomicMin(&d.clo[side][c], f2o(lo[c]));
       atomicMax(&d.chi[side][c], f2o(hi[c]));
@@ -400,20 +473,11 @@ __global__ __launch_bounds__(256) void k_partition(Build B) {
   }
   if (lead < 0) return;
   TaskData& d = B.td[lead];
-  const Task T = B.tasks[lead];
+  const uint32_t lane = threadIdx.x & 63u;
   const bool mine = t == lead;
   for (uint32_t s = 0; s < 2; s++) {
     const bool in = mine && side == s;
-    const uint64_t mask = __ballot(in);
-    if (!mask) continue;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&d.fill[s], (uint32_t)__popcll(mask));
-    base = (uint32_t)__shfl((int)base, 0, 64);
-    if (in) {
-      const uint32_t np = T.b + (s ? d.nl : 0u) + base + lanes_below(mask);
-      B.perm2[np] = q;
-      B.tag[np] = ((uint32_t)lead << 1) | s;
-    }
+    if (!__ballot(in)) continue;
     for (int c = 0; c < 3; c++) {
       const float mn = wmin(in ? lo[c] : INFINITY), mx = wmax(in ? hi[c] : -INFINITY);
       if (lane == 0) {
@@ -424,13 +488,86 @@ __global__ __launch_bounds__(256) void k_partition(Build B) {
   }
 }
 
-// One thread per task: the parent node record and the children's fate
-// (leaf / phase-B subtree / next-level task), as fs_scene.cpp split_into.
+// The fate of side s of task T (fs_scene.cpp split_into): 0 leaf, 1 phase-B
+// subtree, 2 next-level task.
+__device__ __forceinline__ uint32_t fate_of(const Build& B, const Task& T, uint32_t cnt) {
+  if (cnt <= B.leaf || T.depth + 1 >= kGuard) return 0u;
+  return cnt <= kSmall ? 1u : 2u;
+}
+
+// One thread per task: what its two children need (next-level tasks,
+// phase-B subtrees, nodes: one per inner child, cnt - 1 per subtree block).
+__global__ void k_emit_plan(Build B, uint32_t ntasks) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntasks) return;
+  const Task T = B.tasks[t];
+  const TaskData& d = B.td[t];
+  uint32_t next = 0, small = 0, nodes = 0;
+  for (int s = 0; s < 2; s++) {
+    const uint32_t cnt = s ? T.e - T.b - d.nl : d.nl;
+    const uint32_t f = fate_of(B, T, cnt);
+    if (f == 2u) {
+      next++;
+      nodes++;
+    } else if (f == 1u) {
+      small++;
+      nodes += cnt - 1;
+    }
+  }
+  B.plan[t] = make_uint4(next, small, nodes, 0u);
+}
+
+// One block: exclusive scan of the plans in task order, based at the running
+// node and subtree totals (counters[0], [2]); the next level's task count
+// goes to counters[1]. Numbering follows task order, so it is deterministic.
+__global__ __launch_bounds__(1024) void k_emit_scan(Build B, uint32_t ntasks) {
+  __shared__ uint32_t part[3][1024];
+  const uint32_t per = (ntasks + 1023) / 1024, b = threadIdx.x * per, e = min(ntasks, b + per);
+  uint32_t s[3] = {0, 0, 0};
+  for (uint32_t i = b; i < e; i++) {
+    const uint4 v = B.plan[i];
+    s[0] += v.x;
+    s[1] += v.y;
+    s[2] += v.z;
+  }
+  for (int k = 0; k < 3; k++) part[k][threadIdx.x] = s[k];
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    uint32_t y[3] = {0, 0, 0};
+    if (threadIdx.x >= o)
+      for (int k = 0; k < 3; k++) y[k] = part[k][threadIdx.x - o];
+    __syncthreads();
+    for (int k = 0; k < 3; k++) part[k][threadIdx.x] += y[k];
+    __syncthreads();
+  }
+  const uint32_t node0 = B.counters[0], small0 = B.counters[2];
+  uint32_t run[3] = {0, small0, node0};
+  if (threadIdx.x)
+    for (int k = 0; k < 3; k++) run[k] += part[k][threadIdx.x - 1];
+  for (uint32_t i = b; i < e; i++) {
+    const uint4 v = B.plan[i];
+    B.plan[i] = make_uint4(run[0], run[1], run[2], 0u);
+    run[0] += v.x;
+    run[1] += v.y;
+    run[2] += v.z;
+  }
+  __syncthreads();
+  if (threadIdx.x == 1023) {
+    B.counters[1] = part[0][1023];
+    B.counters[2] = small0 + part[1][1023];
+    B.counters[0] = node0 + part[2][1023];
+  }
+}
+
+// One thread per task: the parent node record and the children's records at
+// the scanned offsets (side 0 first), as fs_scene.cpp split_into.
 __global__ void k_emit(Build B, uint32_t ntasks, uint32_t small_max) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntasks) return;
   const Task T = B.tasks[t];
   TaskData& d = B.td[t];
+  const uint4 off = B.plan[t];
+  uint32_t next = off.x, small = off.y, node = off.z;
   atomicMax(&B.counters[3], T.depth);
   atomicAdd(&B.counters[5], 1u);
   for (int s = 0; s < 2; s++) {
@@ -442,12 +579,13 @@ __global__ void k_emit(Build B, uint32_t ntasks, uint32_t small_max) {
     }
     uint32_t word;
     d.child_task[s] = -1;
-    if (cnt <= B.leaf || T.depth + 1 >= kGuard) {
+    const uint32_t f = fate_of(B, T, cnt);
+    if (f == 0u) {
       if (cnt > kMaxLeafCount) atomicOr(&B.counters[4], 1u);
       word = kLeafBit | (cnt << 24) | (B.tri_base + cb);
-    } else if (cnt <= kSmall) {
-      const uint32_t base = atomicAdd(&B.counters[0], cnt - 1);  // a binary tree over cnt: <= cnt-1 inner nodes
-      const uint32_t i = atomicAdd(&B.counters[2], 1u);
+    } else if (f == 1u) {
+      const uint32_t base = node, i = small++;  // a binary tree over cnt: <= cnt-1 inner nodes
+      node += cnt - 1;
       if (base + cnt - 1 > B.max_nodes || i >= small_max) {
         atomicOr(&B.counters[4], 2u);
         word = kLeafBit;
@@ -456,15 +594,14 @@ __global__ void k_emit(Build B, uint32_t ntasks, uint32_t small_max) {
         word = B.node_base + base;
       }
     } else {
-      const uint32_t node = atomicAdd(&B.counters[0], 1u);
-      const uint32_t i = atomicAdd(&B.counters[1], 1u);
-      if (node >= B.max_nodes) {
+      const uint32_t nd = node++, i = next++;
+      if (nd >= B.max_nodes) {
         atomicOr(&B.counters[4], 2u);
         word = kLeafBit;
       } else {
-        B.tasks_next[i] = Task{cb, ce, node, T.depth + 1};
+        B.tasks_next[i] = Task{cb, ce, nd, T.depth + 1};
         d.child_task[s] = (int32_t)i;
-        word = B.node_base + node;
+        word = B.node_base + nd;
       }
     }
     set_child(B.nodes, T.node, s, lo, hi, word);
@@ -749,6 +886,10 @@ int gpu_build_mesh_bvh(hipStream_t stream, const GpuBvhJob& job, BvhNode* d_node
   B.tasks_next = (Task*)alloc(sizeof(Task) * (size_t)max_tasks);
   const uint32_t small_max = 2 * (n / 3 + 2);
   B.small = (Task*)alloc(sizeof(Task) * (size_t)small_max);
+  const uint32_t pblocks = (n + 255) / 256;
+  B.pre = (uint64_t*)alloc(8ull * n);
+  B.bsum = (uint64_t*)alloc(8ull * pblocks);
+  B.plan = (uint4*)alloc(sizeof(uint4) * (size_t)max_tasks);
   B.counters = (uint32_t*)alloc(64);
   for (void* p : allocs)
     if (!p) {
@@ -784,8 +925,11 @@ int gpu_build_mesh_bvh(hipStream_t stream, const GpuBvhJob& job, BvhNode* d_node
     hipLaunchKernelGGL(k_bins, dim3(pg), dim3(256), 0, stream, B);
     hipLaunchKernelGGL(k_split, dim3((ntasks + 63) / 64), dim3(64), 0, stream, B, ntasks);
     hipLaunchKernelGGL(k_select, dim3(ntasks), dim3(256), 0, stream, B);
+    hipLaunchKernelGGL(k_prefix_local, dim3(pg), dim3(256), 0, stream, B);
+    hipLaunchKernelGGL(k_scan_block, dim3(1), dim3(1024), 0, stream, B.bsum, pg);
     hipLaunchKernelGGL(k_partition, dim3(pg), dim3(256), 0, stream, B);
-    GB_HIP(hipMemsetAsync(B.counters + 1, 0, 4, stream));
+    hipLaunchKernelGGL(k_emit_plan, dim3((ntasks + 63) / 64), dim3(64), 0, stream, B, ntasks);
+    hipLaunchKernelGGL(k_emit_scan, dim3(1), dim3(1024), 0, stream, B, ntasks);
     hipLaunchKernelGGL(k_emit, dim3((ntasks + 63) / 64), dim3(64), 0, stream, B, ntasks, small_max);
     hipLaunchKernelGGL(k_retag, dim3(pg), dim3(256), 0, stream, B);
     GB_HIP(hipGetLastError());

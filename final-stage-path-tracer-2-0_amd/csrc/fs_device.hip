@@ -1788,6 +1788,9 @@ int upload(fs_context* ctx, DevBuf* b, const void* src, size_t bytes, size_t ext
   FS_HIP(hipMalloc(&b->p, alloc));
   b->bytes = alloc;
   if (bytes) FS_HIP(hipMemcpyAsync(b->p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  // The tail (device-built slots a build may leave unused, or the placeholder
+  // of an empty array) starts zeroed, so equal uploads are equal bytes.
+  if (alloc > bytes) FS_HIP(hipMemsetAsync((char*)b->p + bytes, 0, alloc - bytes, ctx->stream));
   return FS_OK;
 }
 
@@ -2412,6 +2415,24 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   std::fprintf(stderr, "[fs seq] per-call wave max of lane node visits %llu (node trips %llu), of lane leaf tests "
                "%llu (leaf trips %llu)\n", c.phase[24], c.phase[10], c.phase[25], c.phase[11]);
 #endif
+  return FS_OK;
+}
+
+int fs_scene_digest(fs_context* ctx, uint64_t* digest) {
+  if (!ctx || !digest) return fail(FS_ERR_INVALID, "null argument");
+  if (!ctx->have_scene) return fail(FS_ERR_STATE, "no scene uploaded");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over every device array of the scene
+  std::vector<uint8_t> buf;
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->materials,
+                    &ctx->table, &ctx->tex_rgb, &ctx->tex_info, &ctx->tree, &ctx->tree_objs}) {
+    buf.resize(b->bytes);
+    if (b->bytes) FS_HIP(hipMemcpy(buf.data(), b->p, b->bytes, hipMemcpyDeviceToHost));
+    for (uint8_t v : buf) h = (h ^ v) * 1099511628211ull;
+    for (int k = 0; k < 8; k++) h = (h ^ ((b->bytes >> (8 * k)) & 0xFF)) * 1099511628211ull;
+  }
+  *digest = h;
   return FS_OK;
 }
 

@@ -137,6 +137,7 @@ GPU_SYMBOLS = {
     "fs_frame_unpack": ([_VP, _VP, C.POINTER(fs_render_params), _VP, C.c_size_t], C.c_int),
     "fs_prepare_digest": ([_VP, C.POINTER(fs_options), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                            C.POINTER(C.c_double)], C.c_int),
+    "fs_scene_digest": ([_VP, C.POINTER(C.c_uint64)], C.c_int),
     "fs_trace_range": ([_VP, C.POINTER(fs_camera), C.c_uint32, C.c_uint32, _VP, C.c_uint32, _VP], C.c_int),
 }
 HOST_SYMBOLS = {
@@ -429,6 +430,12 @@ class Renderer:
                                         C.byref(m)), "fs_scene_stats")
         return {"build_ms": b.value, "upload_ms": u.value, "triangles": t.value, "nodes": n.value,
                 "device_bytes": m.value}
+
+    def scene_digest(self):
+        """fs_scene_digest: FNV-1a of every device array of the uploaded scene."""
+        d = C.c_uint64()
+        _check(gpu_lib().fs_scene_digest(self.ctx, C.byref(d)), "fs_scene_digest")
+        return d.value
 
     def frame(self, width, height):
         return Frame(self, width, height)

@@ -332,6 +332,12 @@ int fs_frame_unpack(fs_context* ctx, fs_frame* frame, const fs_render_params* pa
 int fs_prepare_digest(const fs_scene_desc* desc, const fs_options* opt, uint64_t* digest, uint64_t* num_nodes,
                       double* build_ms);
 
+/* 64-bit digest of every device array of the uploaded scene (objects, BVH
+ * nodes, triangles, normals, texcoords, materials, table, textures, object
+ * octree), including the device-built BVHs: equal uploads give equal
+ * digests (build reproducibility checks). Synchronous. */
+int fs_scene_digest(fs_context* ctx, uint64_t* digest);
+
 /* ---- TraceRange (engine.cpp:298-329) ------------------------------------
  * Focus pick: for each of `count` image points (x, y interleaved in xy) of a
  * width x height frame, the distance from camera->origin to the first hit of
