@@ -346,6 +346,7 @@ __device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, 
 template <bool COUNT>
 struct Tally {
   uint32_t nodes = 0, tris = 0, prims = 0;
+  uint32_t objs = 0;  // object records read (wave-uniform loads: counted once per wave)
 #ifdef FS_PHASE_PROF
   // wave-level loop trips, counted by the first active lane of each trip
   uint32_t node_trips = 0, leaf_trips = 0, lane_nodes = 0, lane_leaves = 0;
@@ -826,6 +827,7 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
   const DevObject* __restrict__ o = S.objects + oi;
   const float* d = o->d;
   const int32_t kind = o->kind;
+  if (COUNT) tally.objs++;  // per-lane object index: a vector load per lane
   if (kind == FS_OBJ_MESH) {
     if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) return false;
     const int32_t before = h.obj;
@@ -1025,6 +1027,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
     if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
+    if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
     int32_t kind = o->kind;
     const __attribute__((address_space(4))) float* d = o->d;
     if (kind == FS_OBJ_MESH) {
@@ -1271,10 +1274,107 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
   if (plane_dist(cp, r.start) < 0.0f) n = n * (float)-1.0;
 }
 
-// Path regeneration with a lean register footprint: the closest-hit query
-// keeps only (t, object, primitive, u, v); the per-bounce shading scalars
-// and the Fog anchors live in a per-lane HBM scratch row, and the depth-0
-// AOVs go straight to the frame. Same outputs as render_kernel_regen.
+// One block of (pixel, sample) tasks: an 8x8 micro-tile of one sample group
+// (wave-uniform, lives in SGPRs). Block b of a launch of nblocks decodes as
+// a one-shot launch's blockIdx.x = b did: tile-major or group-major order,
+// the centre-first tile order, and the XCD placement (block b belongs to
+// XCD b & 7, the hardware's round-robin of workgroups over the 8 XCDs).
+struct TaskBlock {
+  uint32_t x0 = 0, y0 = 0, vx = 0, nvalid = 1;
+  uint32_t total = 0, next = 0;  // tasks (in-frame pixels x spp) and the next one to hand out
+  uint32_t rad_row = 0;          // radiance row (group * owned + tile) * micro-tiles + micro-tile
+  uint32_t sample0 = 0;          // sample index of the group's first sample
+  bool aov = false;              // last group: its last sample leaves the AOV planes
+};
+
+__device__ __forceinline__ TaskBlock decode_block(const Launch& P, const DevFrame& F, uint32_t b) {
+  const uint32_t micro_per_side = P.tile_size / 8;
+  const uint32_t micro_per_tile = micro_per_side * micro_per_side;
+  // xcd_bands 2 gives each XCD whole 64x64 tiles, so one L2 serves the rays
+  // of a tile; 1 (one band per XCD) is kept for A/B runs.
+  if (P.xcd_bands == 1) {
+    const uint32_t per = P.nblocks >> 3, rem = P.nblocks & 7u, xcd = b & 7u, k = b >> 3;
+    b = xcd < rem ? xcd * (per + 1) + k : rem * (per + 1) + (xcd - rem) * per + k;
+  } else if (P.xcd_bands == 2) {  // whole tiles per XCD: tile 8j + x on XCD x
+    const uint32_t groups = P.nblocks / (8 * micro_per_tile);  // full groups of 8 tiles
+    const uint32_t xcd = b & 7u, k = b >> 3;
+    if (k < groups * micro_per_tile) b = ((k / micro_per_tile) * 8 + xcd) * micro_per_tile + k % micro_per_tile;
+  }
+  // a virtual tile list of owned tiles x groups, tile-major (a tile's groups
+  // run together: the resident waves cover few tiles) or, with group_major,
+  // group-major
+  const uint32_t vtile = b / micro_per_tile, micro = b % micro_per_tile;
+  uint32_t t, group;
+  if (P.group_major) {
+    group = vtile / P.owned;
+    t = vtile - group * P.owned;
+  } else {
+    t = vtile / P.groups;
+    group = vtile - t * P.groups;
+  }
+  if (P.tile_order) t = P.tile_order[t];
+  TaskBlock B;
+  B.rad_row = (group * P.owned + t) * micro_per_tile + micro;
+  const uint32_t tile = P.tile_offset + t * P.tile_stride;
+  const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  B.x0 = tx * P.tile_size + (micro % micro_per_side) * 8;
+  B.y0 = ty * P.tile_size + (micro / micro_per_side) * 8;
+  B.sample0 = P.sample_base + group * P.spp;
+  B.aov = group + 1 == P.groups;
+  B.next = 0;
+  if (B.x0 < F.width && B.y0 < F.height) {  // only in-frame pixels are enumerated
+    B.vx = min(8u, F.width - B.x0);
+    B.nvalid = B.vx * min(8u, F.height - B.y0);
+    B.total = B.nvalid * P.spp;
+  } else {
+    B.vx = 1;
+    B.nvalid = 1;
+    B.total = 0;
+  }
+  return B;
+}
+
+constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+constexpr uint32_t kQueueStride = 64;  // work-queue counters 256 B apart
+
+// The wave's next block. One-shot waves (P.persist 0) take block
+// blockIdx.x once. Persistent waves pull blocks b = 8i + x from the queue of
+// their own XCD x (wave w runs on XCD w & 7), so a block keeps the XCD (and
+// L2) the one-shot placement gives it; when that queue is empty they take
+// blocks of the other XCDs' queues in turn. One lane performs the atomic.
+__device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __restrict__ queues, uint32_t& q,
+                                                uint32_t& left) {
+  if (!P.persist) {
+    const uint32_t b = left ? (uint32_t)blockIdx.x : kNoBlock;
+    left = 0;
+    return b;
+  }
+  while (left) {
+    uint32_t i = 0;
+    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) i = atomicAdd(queues + q * kQueueStride, 1u);
+    i = (uint32_t)__builtin_amdgcn_readfirstlane(i);
+    const uint64_t b = (uint64_t)i * 8u + q;
+    if (b < P.nblocks) return (uint32_t)b;
+    q = (q + 1) & 7u;
+    left--;
+  }
+  return kNoBlock;
+}
+
+// The path-trace megakernel: path regeneration with a lean register
+// footprint. The closest-hit query keeps only (t, object, primitive, u, v);
+// the per-bounce shading scalars and the Fog anchors live in per-lane HBM
+// scratch rows of the wave; the depth-0 AOVs go straight to the frame.
+//
+// Work: the wave's lanes share one pool of (pixel, sample) tasks. Whenever
+// lanes are free (their path ended) they take the next tasks of the wave's
+// current block in sample-major order (ballot + mbcnt, no atomics), and
+// when the block runs dry the wave fetches the next block and goes on
+// handing out its tasks, so lanes never wait for a block's stragglers. With
+// P.persist the grid is one wave per wave slot of the chip and the waves
+// pull blocks until every queue is empty: the launch tail is one task
+// path, not one block. Each sample's radiance goes to its block's radiance
+// row; fold_groups folds the rows into the frame in sample order.
 template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
@@ -1282,74 +1382,27 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
                                                                      float4* __restrict__ tex_all,
                                                                      float* __restrict__ rad_all,
                                                                      uint32_t* __restrict__ mat_all,
+                                                                     uint32_t* __restrict__ queues,
                                                                      DevCounters* __restrict__ counters) {
   __shared__ uint32_t stk_all[kTraversalStack * kBlock];
   const uint32_t lane = threadIdx.x;
   uint32_t* stk = stk_all + lane;
-  // Scratch rows, depth-major per wave ([level][lane]) so a wave's store is
-  // one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
+  // Scratch rows of the wave, depth-major ([level][lane]) so a wave's store
+  // is one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
   float2* lvl = lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
   float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
   float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
 
-  uint32_t x0, y0;  // the wave's 8x8 pixel micro-tile
-  uint32_t group = 0, rad_row = blockIdx.x;  // sample group; radiance row (g * micro-tiles + micro-tile)
-  {
-    const uint32_t micro_per_side = P.tile_size / 8;
-    const uint32_t micro_per_tile = micro_per_side * micro_per_side;
-    // Blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one L2).
-    // xcd_bands 2 gives each XCD whole 64x64 tiles, so one L2 serves the rays
-    // of a tile; 1 (one band per XCD) is kept for A/B runs.
-    uint32_t b = blockIdx.x;
-    if (P.xcd_bands == 1) {
-      const uint32_t per = gridDim.x >> 3, rem = gridDim.x & 7u, xcd = b & 7u, k = b >> 3;
-      b = xcd < rem ? xcd * (per + 1) + k : rem * (per + 1) + (xcd - rem) * per + k;
-    } else if (P.xcd_bands == 2) {  // whole tiles per XCD: tile 8j + x on XCD x
-      const uint32_t groups = gridDim.x / (8 * micro_per_tile);  // full groups of 8 tiles
-      const uint32_t xcd = b & 7u, k = b >> 3;
-      if (k < groups * micro_per_tile) b = ((k / micro_per_tile) * 8 + xcd) * micro_per_tile + k % micro_per_tile;
-    }
-    // a virtual tile list of owned tiles x groups, tile-major (a tile's
-    // groups run together: the resident waves cover few tiles) or, with
-    // group_major, group-major
-    const uint32_t vtile = b / micro_per_tile, micro = b % micro_per_tile;
-    uint32_t t;
-    if (P.group_major) {
-      group = vtile / P.owned;
-      t = vtile - group * P.owned;
-    } else {
-      t = vtile / P.groups;
-      group = vtile - t * P.groups;
-    }
-    if (P.tile_order) t = P.tile_order[t];
-    rad_row = (group * P.owned + t) * micro_per_tile + micro;
-    const uint32_t tile = P.tile_offset + t * P.tile_stride;
-    const uint32_t tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    x0 = tx * P.tile_size + (micro % micro_per_side) * 8;
-    y0 = ty * P.tile_size + (micro / micro_per_side) * 8;
-  }
-  const uint64_t sample_base = (uint64_t)P.sample_base + (uint64_t)group * P.spp;
-  const bool last_group = group + 1 == P.groups;
-  uint32_t x = x0 + (lane & 7), y = y0 + (lane >> 3);
-  const bool own_valid = x < F.width && y < F.height;
-  if (x0 >= F.width || y0 >= F.height) return;  // whole micro-tile outside the frame
-  uint32_t pix = y * F.width + x;
+  TaskBlock cur;  // the block the wave hands out tasks from
+  uint32_t queue = blockIdx.x & 7u, queues_left = P.persist ? 8u : 1u;
   Tally<COUNT> tally;
-  uint32_t segments = 0;
-  // The wave's kBlock x spp (pixel, sample) tasks are taken in
-  // sample-major order from a wave-uniform counter by whichever lane is
-  // free; each sample's radiance goes to a scratch row and every pixel folds
-  // its samples in order at the end (same running-mean rounding).
-  float* rad = rad_all + (size_t)rad_row * (3 * kChunk * kBlock);
-  uint32_t next_task = 0;
-  // only the micro-tile's in-frame pixels (vx x vy) are enumerated, so every
-  // task is real work and the loop has no early continue
-  const uint32_t vx = min(8u, F.width - x0), vy = min(8u, F.height - y0), nvalid = vx * vy;
-  const uint32_t total_tasks = nvalid * P.spp;
-  uint32_t task_lp = lane;
+  uint32_t segments = 0, samples_done = 0;
 
-  uint32_t s = 0;
+  // the lane's task: its pixel, sample and radiance slot
+  uint32_t x = 0, y = 0, pix = 0, smp = 0;
+  uint32_t rad_row = 0;
+  uint32_t slot = 0;  // s * kBlock + 8 * py + px, bit 31: this sample leaves the AOVs
   uint64_t rng = 0;
   Ray r;
   uint32_t depth = 0;
@@ -1377,22 +1430,42 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   for (;;) {
     FS_PHASE(0);
     {
+      // Hand the free lanes their next tasks, in lane order, from the
+      // current block and, when it runs dry, from the blocks fetched after
+      // it. Every update of `cur` is wave-uniform; the loop has no early
+      // exits other than the final break of lanes left without work.
       const uint64_t m = __ballot(fresh);
-      if (fresh) {
-        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        uint32_t task = next_task + rank;
-        if (task >= total_tasks) break;  // this lane is done
-        s = task / nvalid;
-        const uint32_t k = task - s * nvalid, px = k % vx, py = k / vx;
-        task_lp = py * 8 + px;
-        x = x0 + px;
-        y = y0 + py;
-        pix = y * F.width + x;
+      const uint32_t nfree = (uint32_t)__popcll(m);
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      bool got = false;
+      uint32_t served = 0;
+      while (served < nfree) {
+        if (cur.next >= cur.total) {
+          const uint32_t b = fetch_block(P, queues, queue, queues_left);
+          if (b == kNoBlock) break;
+          cur = decode_block(P, F, b);
+        } else {
+          const uint32_t take = min(nfree - served, cur.total - cur.next);
+          if (fresh && rank - served < take) {
+            const uint32_t task = cur.next + (rank - served);
+            const uint32_t s = task / cur.nvalid;
+            const uint32_t k = task - s * cur.nvalid, px = k % cur.vx, py = k / cur.vx;
+            x = cur.x0 + px;
+            y = cur.y0 + py;
+            pix = y * F.width + x;
+            smp = cur.sample0 + s;
+            rad_row = cur.rad_row;
+            slot = (s * kBlock + py * 8 + px) | ((cur.aov && s == P.spp - 1) ? 0x80000000u : 0u);
+            got = true;
+          }
+          cur.next += take;
+          served += take;
+        }
       }
-      next_task += (uint32_t)__popcll(m);
+      if (fresh && !got) break;  // every queue is empty: this lane is done
     }
     if (fresh) {
-      rng = pixel_seed(pix, sample_base + s, P.seed);
+      rng = pixel_seed(pix, smp, P.seed);
       r = camera_ray(C, (float)x, (float)y, rng);
       depth = 0;
       mats.reset();
@@ -1402,6 +1475,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       fresh = false;
     }
     FS_PHASE(1);
+    const bool aov = (slot >> 31) != 0;
     bool done = false;
     f3 L = mk3(0, 0, 0);
     if (depth >= kMaxDepth) {
@@ -1457,7 +1531,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           sphere_tc(normalize(r.stop - r.start), tu, tv);
           L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
         }
-        if (depth == 0 && last_group && s == P.spp - 1) {  // the last sample's AOVs remain
+        if (depth == 0 && aov) {  // the last sample's AOVs remain
           f3 nd = normalize(r.dir);
           at_byte(F.normal, pix * 12u)[0] = nd.x;
           at_byte(F.normal, pix * 12u)[1] = nd.y;
@@ -1490,7 +1564,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
-        if (depth == 0 && last_group && s == P.spp - 1) {
+        if (depth == 0 && aov) {
           at_byte(F.normal, pix * 12u)[0] = nn.x;
           at_byte(F.normal, pix * 12u)[1] = nn.y;
           at_byte(F.normal, pix * 12u)[2] = nn.z;
@@ -1521,10 +1595,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX, MMAT>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      const uint32_t o = s * kBlock + task_lp;
+      float* rad = rad_all + (size_t)rad_row * (3 * kChunk * kBlock);
+      const uint32_t o = slot & 0x7FFFFFFFu;
       rad[o] = L.x;
       rad[kChunk * kBlock + o] = L.y;
       rad[2 * kChunk * kBlock + o] = L.z;
+      if (COUNT) samples_done++;
       fresh = true;
     }
     FS_PHASE(4);
@@ -1542,43 +1618,22 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   atomicAdd(&counters->phase[13], (unsigned long long)tally.lane_leaves);
 #endif
 #undef FS_PHASE
-  __syncthreads();  // the wave's radiance rows are complete and visible
-  if (COUNT) {  // every lane's work; samples once per in-frame pixel
-    if (own_valid) atomicAdd(&counters->samples, (unsigned long long)P.spp);
+  if (COUNT) {  // every lane's work
+    atomicAdd(&counters->samples, (unsigned long long)samples_done);
     atomicAdd(&counters->segments, (unsigned long long)segments);
     atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
     atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
     atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
+    atomicAdd(&counters->object_loads, (unsigned long long)tally.objs);
   }
-  if (!own_valid) return;
-  if (P.groups > 1) return;  // fold_groups folds every group's rows in sample order
-  x = x0 + (lane & 7);
-  y = y0 + (lane >> 3);
-  pix = y * F.width + x;
-  f3 mean = mk3(F.color[3 * (size_t)pix], F.color[3 * (size_t)pix + 1], F.color[3 * (size_t)pix + 2]);
-  uint32_t n = F.count[pix];
-  for (uint32_t k = 0; k < P.spp; k++) {  // frame.cpp:53-63, samples in order
-    const uint32_t o = k * kBlock + lane;
-    f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
-    f3 np = mean * (float)n + L;
-    float dv = (float)(++n);
-    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
-  }
-  F.color[3 * (size_t)pix] = mean.x;
-  F.color[3 * (size_t)pix + 1] = mean.y;
-  F.color[3 * (size_t)pix + 2] = mean.z;
-  F.count[pix] = n;
-  F.display[3 * (size_t)pix] = gamma8(mean.x);
-  F.display[3 * (size_t)pix + 1] = gamma8(mean.y);
-  F.display[3 * (size_t)pix + 2] = gamma8(mean.z);
 }
 
-// Folds the radiance rows of a launch with P.groups > 1 into the frame:
-// block b is micro-tile b of group 0 (same decode as render_kernel_lean with
-// xcd_bands 0), lane = pixel; group g's rows are row g * gridDim.x + b. Each
-// pixel folds its samples in sample order (frame.cpp:53-63), so the frame is
-// bit-identical to groups x spp consecutive single-group launches. HBM-bound:
-// 12 B read per sample plus one frame row.
+// Folds the radiance rows of a launch into the frame: block b is micro-tile
+// b of group 0 (decode_block's tile-major order without the XCD placement
+// or tile order), lane = pixel; group g's rows are row g * gridDim.x + b.
+// Each pixel folds its samples in sample order (frame.cpp:53-63), so the
+// frame is bit-identical to groups x spp consecutive TraceScene calls.
+// HBM-bound: 12 B read per sample plus one frame row.
 __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, const float* __restrict__ rad_all) {
   const uint32_t lane = threadIdx.x, b = blockIdx.x;
   const uint32_t micro_per_side = P.tile_size / 8, micro_per_tile = micro_per_side * micro_per_side;
@@ -1765,6 +1820,8 @@ struct fs_context {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf rows;  // per-lane scratch rows of the lean kernel (LeanRows)
+  DevBuf queues;  // per-XCD work-queue counters of the persistent trace kernel
+  uint32_t cus = 0;  // compute units: the persistent grid is one wave per wave slot
 };
 
 struct fs_frame {
@@ -1839,9 +1896,10 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
   return b;
 }
 
-// Per-lane scratch rows of the lean kernel, carved out of one allocation:
-// the shading scalars (lvl), the Fog anchors, texel rows (textured scenes)
-// and the radiance rows of the pooled samples.
+// Scratch of the lean kernel, carved out of one allocation: per wave of the
+// grid, the per-lane rows of the shading scalars (lvl), the Fog anchors, the
+// texels (textured scenes) and the material ids (MMAT); per block of the
+// launch, the radiance rows of its samples (read by fold_groups).
 struct LeanRows {
   float2* lvl = nullptr;
   float4* anchor = nullptr;
@@ -1849,9 +1907,9 @@ struct LeanRows {
   float* rad = nullptr;
   uint32_t* mat = nullptr;
 };
-int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows, bool mat_rows) {
-  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + 12 * kChunk + (mat_rows ? 4 * kMaxDepth : 0);
-  const size_t bytes = (size_t)slots * per + 5 * 256;  // + alignment of each array
+int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, LeanRows* W, bool tex_rows, bool mat_rows) {
+  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + (mat_rows ? 4 * kMaxDepth : 0);
+  const size_t bytes = (size_t)wave_lanes * per + (size_t)block_lanes * 12 * kChunk + 5 * 256;  // + alignment
   if (ctx->rows.bytes < bytes) {
     int rc = ensure(&ctx->rows, bytes);
     if (rc) return rc;
@@ -1863,11 +1921,11 @@ int lean_rows(fs_context* ctx, uint32_t slots, LeanRows* W, bool tex_rows, bool 
     return q;
   };
   *W = LeanRows{};
-  W->anchor = (float4*)take(32ull * slots);
-  W->lvl = (float2*)take(8ull * kMaxDepth * slots);
-  W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * slots) : nullptr;
-  W->rad = (float*)take(12ull * kChunk * slots);
-  W->mat = mat_rows ? (uint32_t*)take(4ull * kMaxDepth * slots) : nullptr;
+  W->anchor = (float4*)take(32ull * wave_lanes);
+  W->lvl = (float2*)take(8ull * kMaxDepth * wave_lanes);
+  W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * wave_lanes) : nullptr;
+  W->rad = (float*)take(12ull * kChunk * block_lanes);
+  W->mat = mat_rows ? (uint32_t*)take(4ull * kMaxDepth * wave_lanes) : nullptr;
   if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
   return FS_OK;
 }
@@ -1938,10 +1996,11 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 // walks), MMAT (material ids in scratch rows)>. Textured scenes never park.
 // Names as rocprofv3 prints the uncounted ones (fs_last_kernel).
 typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, float2*, float4*, float4*, float*, uint32_t*,
-                       DevCounters*);
+                       uint32_t*, DevCounters*);
 struct LeanKernel {
   LeanFn fn;
   const char* name;
+  uint32_t waves;  // waves per SIMD (__launch_bounds__)
 };
 template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false>
 LeanKernel lean_kernel(bool count) {
@@ -1951,7 +2010,7 @@ LeanKernel lean_kernel(bool count) {
                                   (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ">";
   return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT>
                 : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT>,
-          name.c_str()};
+          name.c_str(), (uint32_t)W};
 }
 // Scenes traced through the object octree take one instantiation that covers
 // textures and any material count (their object loop is per lane anyway).
@@ -1969,6 +2028,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..127";
   else if (o->bvh_bins < 2 || o->bvh_bins > 64) *why = "bvh_bins must be 2..64";
   else if (o->node_layout > FS_NODE_LAYOUT_PAIRS) *why = "unknown node_layout";
+  else if (o->persist > 1) *why = "persist must be 0 or 1";
   else return true;
   return false;
 }
@@ -2004,6 +2064,11 @@ int fs_create(int device, fs_context** out) {
   FS_HIP(hipMalloc(&ctx->counters.p, sizeof(DevCounters)));
   ctx->counters.bytes = sizeof(DevCounters);
   FS_HIP(hipMemset(ctx->counters.p, 0, sizeof(DevCounters)));
+  int cus = 0;
+  FS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  ctx->cus = cus > 0 ? (uint32_t)cus : 1u;
+  FS_HIP(hipMalloc(&ctx->queues.p, 8 * dev::kQueueStride * sizeof(uint32_t)));
+  ctx->queues.bytes = 8 * dev::kQueueStride * sizeof(uint32_t);
   *out = ctx.release();
   return FS_OK;
 }
@@ -2015,7 +2080,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
-                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order})
+                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
   ctx->rows.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -2042,6 +2107,7 @@ int fs_options_default(fs_options* o) {
   o->bvh_threads = 0;
   o->node_layout = FS_NODE_LAYOUT_DEPTH_FIRST;
   o->build_log = 0;
+  o->persist = 1;
   return FS_OK;
 }
 
@@ -2339,20 +2405,29 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   LeanRows rows;
   const bool tree = ctx->scene.tree != nullptr;
   const bool mm = ctx->many_materials || tree;
-  if (blocks && (rc = lean_rows(ctx, (uint32_t)(blocks * G * kBlock), &rows, ctx->has_textures || tree, mm))) return rc;
   const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr);
+  // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
+  // K.waves waves per SIMD), never more than the launch has blocks.
+  const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
+  const uint64_t max_grid = O.persist ? std::min<uint64_t>(wave_slots, blocks * G) : blocks * G;
+  if (blocks * G >= (1ull << 31)) return fail(FS_ERR_INVALID, "render too large for one launch (blocks x groups >= 2^31)");
+  if (blocks && (rc = lean_rows(ctx, max_grid * kBlock, blocks * G * kBlock, &rows, ctx->has_textures || tree, mm)))
+    return rc;
   ctx->last_kernel = K.name;
+  L.persist = O.persist;
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
     L.groups = L.spp == chunk ? std::min(G, (params->spp - done) / chunk) : 1u;
+    L.nblocks = (uint32_t)(blocks * L.groups);
     done += L.groups * L.spp;
     ctx->last_launches++;
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
-    hipLaunchKernelGGL(K.fn, dim3((uint32_t)(blocks * L.groups)), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L,
-                       rows.lvl, rows.anchor, rows.tex, rows.rad, rows.mat, (DevCounters*)ctx->counters.p);
-    if (L.groups > 1)
-      hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
+    const uint32_t grid = (uint32_t)(O.persist ? std::min<uint64_t>(wave_slots, L.nblocks) : L.nblocks);
+    if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
+    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
+                       rows.tex, rows.rad, rows.mat, (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
+    hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -2398,6 +2473,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->node_visits = c.node_visits;
   out->tri_tests = c.tri_tests;
   out->prim_tests = c.prim_tests;
+  out->object_loads = c.object_loads;
 #ifdef FS_PHASE_PROF
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "

@@ -1,4 +1,5 @@
-// fs_kernels.h — device code of the hot path (one wave64 per 8x8 pixel block).
+// fs_kernels.h — device code of the hot path (one wave64 per workgroup; a
+// block of work is one 8x8 pixel micro-tile of a sample group).
 //
 // Restates, per sample, engine.cpp:59-251 (ray generation, TraceStep),
 // scene.cpp:227-249 (closest hit + back-face flip), object.cpp / intersect.cpp
@@ -67,7 +68,7 @@ struct DevFrame {
 };
 
 struct DevCounters {
-  unsigned long long samples, segments, node_visits, tri_tests, prim_tests;
+  unsigned long long samples, segments, node_visits, tri_tests, prim_tests, object_loads;
   // Per-wave cycle totals by loop phase; filled only by -DFS_PHASE_PROF
   // builds (libfsgpu_prof.so, a measurement tool, never the product path).
   unsigned long long phase[32];
@@ -91,6 +92,8 @@ struct Launch {
   // radiance rows, so frames are identical.
   const uint32_t* tile_order;
   uint64_t seed;
+  uint32_t nblocks;  // blocks of the launch: owned tiles x micro-tiles x groups
+  uint32_t persist;  // 1: persistent waves pull blocks from per-XCD queues; 0: one wave per block
 };
 
 }  // namespace fs

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 2
+#define FS_ABI_VERSION 3
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -206,7 +206,9 @@ typedef struct fs_counters {
   uint64_t segments;    /* ray segments traced (closest-hit queries) */
   uint64_t node_visits; /* BVH nodes whose boxes were tested */
   uint64_t tri_tests;   /* ray/triangle tests */
-  uint64_t prim_tests;  /* analytic object tests */
+  uint64_t prim_tests;  /* analytic object tests (per lane) */
+  uint64_t object_loads; /* object records read: wave-uniform scalar loads, one per
+                            wave per object visit of a closest-hit query */
 } fs_counters;
 
 typedef struct fs_context fs_context;
@@ -244,6 +246,8 @@ typedef struct fs_options {
   uint32_t bvh_threads;        /* host BVH build threads, 0 = 16 (0) */
   uint32_t node_layout;        /* FS_NODE_LAYOUT_* of host-built trees (DEPTH_FIRST) */
   uint32_t build_log;          /* 1: scene build phases to stderr (0) */
+  uint32_t persist;            /* 1 persistent waves pulling blocks from per-XCD queues (1),
+                                  0 one wave per block */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */

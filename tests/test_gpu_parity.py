@@ -560,6 +560,8 @@ OPTION_VARIANTS = [
     {"node_layout": "pairs"},
     {"bvh_leaf": 5, "bvh_bins": 7},
     {"bvh_threads": 1},
+    {"persist": 0},
+    {"persist": 0, "samples_per_block": 7, "groups": 3},
 ]
 
 
