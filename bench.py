@@ -46,10 +46,12 @@ WORKLOADS = {
     "c3": "~250k-triangle procedural atrium (BASELINE configs[2]) at 1920x1080, 1024 spp",
 }
 # Algorithmic bytes per unit of work, from the device SoA record
-# sizes: BVH node 64 B, triangle 64 B (fs_scene.h DevTri), analytic object record 128 B, per
-# segment one material record (76 B) + one normal-table entry (16 B); per
-# sample 12 B of radiance.
-S_NODE, S_TRI, S_PRIM, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
+# sizes: BVH node 64 B and triangle 64 B (fs_scene.h DevTri), both per lane;
+# an object record 128 B per WAVE (the object loop reads records with scalar
+# loads at a wave-uniform index: one load serves the 64 lanes); per segment
+# one material record (76 B) + one normal-table entry (16 B); per sample 12 B
+# of radiance.
+S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
 
 
 def parse():
@@ -148,7 +150,7 @@ def main():
     r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
     c = r.counters()
     cf.close()
-    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * c["tri_tests"] + S_PRIM * c["prim_tests"]
+    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * c["tri_tests"] + S_OBJ * c["object_loads"]
                         + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
     avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
     owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
@@ -165,12 +167,17 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                # the same launch time against the PMC-measured bytes (FETCH x2 + WRITE per launch)
+                "traffic_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic else None,
+                "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                 "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "launches_per_step": launches, "spp_per_launch": launch_spp,
                 "bytes_per_sample": round(bytes_per_sample, 1),
                 "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
                 "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),
-                "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2)}
+                "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2),
+                "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
+                "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

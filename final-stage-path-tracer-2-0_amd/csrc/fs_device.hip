@@ -1595,11 +1595,11 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX, MMAT>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      float* rad = rad_all + (size_t)rad_row * (3 * kChunk * kBlock);
+      float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);  // [channel][sample][pixel]
       const uint32_t o = slot & 0x7FFFFFFFu;
       rad[o] = L.x;
-      rad[kChunk * kBlock + o] = L.y;
-      rad[2 * kChunk * kBlock + o] = L.z;
+      rad[P.spp * kBlock + o] = L.y;
+      rad[2 * P.spp * kBlock + o] = L.z;
       if (COUNT) samples_done++;
       fresh = true;
     }
@@ -1646,10 +1646,10 @@ __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, cons
   f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
   uint32_t n = F.count[pix];
   for (uint32_t g = 0; g < P.groups; g++) {
-    const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * kChunk * kBlock);
+    const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * P.spp * kBlock);
     for (uint32_t k = 0; k < P.spp; k++) {
       const uint32_t o = k * kBlock + lane;
-      f3 L = mk3(rad[o], rad[kChunk * kBlock + o], rad[2 * kChunk * kBlock + o]);
+      f3 L = mk3(rad[o], rad[P.spp * kBlock + o], rad[2 * P.spp * kBlock + o]);
       f3 np = mean * (float)n + L;
       float dv = (float)(++n);
       mean = mk3(np.x / dv, np.y / dv, np.z / dv);
@@ -1907,9 +1907,10 @@ struct LeanRows {
   float* rad = nullptr;
   uint32_t* mat = nullptr;
 };
-int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, LeanRows* W, bool tex_rows, bool mat_rows) {
+int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, uint32_t spp, LeanRows* W, bool tex_rows,
+              bool mat_rows) {
   const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + (mat_rows ? 4 * kMaxDepth : 0);
-  const size_t bytes = (size_t)wave_lanes * per + (size_t)block_lanes * 12 * kChunk + 5 * 256;  // + alignment
+  const size_t bytes = (size_t)wave_lanes * per + (size_t)block_lanes * 12 * spp + 5 * 256;  // + alignment
   if (ctx->rows.bytes < bytes) {
     int rc = ensure(&ctx->rows, bytes);
     if (rc) return rc;
@@ -1924,7 +1925,7 @@ int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, LeanRo
   W->anchor = (float4*)take(32ull * wave_lanes);
   W->lvl = (float2*)take(8ull * kMaxDepth * wave_lanes);
   W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * wave_lanes) : nullptr;
-  W->rad = (float*)take(12ull * kChunk * block_lanes);
+  W->rad = (float*)take(12ull * spp * block_lanes);
   W->mat = mat_rows ? (uint32_t*)take(4ull * kMaxDepth * wave_lanes) : nullptr;
   if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
   return FS_OK;
@@ -2096,7 +2097,7 @@ int fs_options_default(fs_options* o) {
   o->schedule = FS_SCHEDULE_AUTO;
   o->park_lanes = 10;  // C4: 8-10 best at 6 waves per SIMD
   o->park_min_tris = kParkMinTris;
-  o->samples_per_block = kChunk;
+  o->samples_per_block = 16;  // persistent waves: C4 +0.7 %, C3 +2 %, C2 +3 % over 64 (8 and 4 no better)
   o->groups = 0;
   o->group_major = 0;
   o->tile_order = 1;
@@ -2342,8 +2343,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
   // Long renders are split into launches of sample groups of `chunk` samples
   // per pixel; the running mean lives in the frame, so the result is
-  // identical. The kernel takes any per-block count up to kChunk (the
-  // radiance rows keep the kChunk stride).
+  // identical. A block takes any per-block count up to kChunk; its radiance
+  // row holds 3 x spp x 64 floats.
   const uint32_t chunk = O.samples_per_block;
   // Schedule (every schedule produces identical frames): LEAN, the
   // path-regeneration megakernel with the unwind scratch in HBM rows,
@@ -2358,15 +2359,18 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
   // Sample groups: a launch renders G runs of `chunk` samples as
-  // G x blocks blocks, then fold_groups folds them in order. G is sized so a
-  // launch holds >= kGroupTargetBlocks blocks (about 43 per wave slot of the
-  // chip), which makes the launch tail small and keeps the CUs full when a
-  // multi-GPU rank owns few tiles.
+  // G x blocks blocks, then fold_groups folds them in order. Persistent
+  // waves have a launch tail of one task path, so G is as large as the
+  // radiance rows allow (kRadianceRowBytes: C4 at 1080p x 1024 spp is one
+  // launch, 25.7 GB of rows). One-shot waves size G so a launch holds
+  // >= kGroupTargetBlocks blocks (about 43 per wave slot of the chip).
   const uint32_t full_chunks = params->spp / chunk;
   uint32_t G = 1;
   if (blocks && full_chunks > 1) {
-    uint64_t want = O.groups ? (uint64_t)O.groups : (kGroupTargetBlocks + blocks - 1) / blocks;
-    want = std::min<uint64_t>(want, full_chunks);
+    uint64_t want = O.groups  ? (uint64_t)O.groups
+                    : O.persist ? std::max<uint64_t>(1, kRadianceRowBytes / (blocks * 12ull * chunk * kBlock))
+                                : (kGroupTargetBlocks + blocks - 1) / blocks;
+    want = std::max<uint64_t>(1, std::min<uint64_t>({want, full_chunks, ((1ull << 31) - 1) / blocks}));
     const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
     G = (full_chunks + nl - 1) / nl;                                   // balanced groups per launch
   }
@@ -2410,8 +2414,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // K.waves waves per SIMD), never more than the launch has blocks.
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
   const uint64_t max_grid = O.persist ? std::min<uint64_t>(wave_slots, blocks * G) : blocks * G;
-  if (blocks * G >= (1ull << 31)) return fail(FS_ERR_INVALID, "render too large for one launch (blocks x groups >= 2^31)");
-  if (blocks && (rc = lean_rows(ctx, max_grid * kBlock, blocks * G * kBlock, &rows, ctx->has_textures || tree, mm)))
+  if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
+  if (blocks && (rc = lean_rows(ctx, max_grid * kBlock, blocks * G * kBlock, chunk, &rows, ctx->has_textures || tree, mm)))
     return rc;
   ctx->last_kernel = K.name;
   L.persist = O.persist;

@@ -28,6 +28,9 @@ constexpr uint32_t kPackedMaterials = 255;
 // of 512 spp, +2.6 % over 4 launches of 256 — a launch ends with a tail of
 // about one block's duration).
 constexpr uint64_t kGroupTargetBlocks = 262144;
+// Persistent launches: sample groups per launch up to this many bytes of
+// radiance rows (12 B per sample; of 288 GB of HBM).
+constexpr uint64_t kRadianceRowBytes = 32ull << 30;
 
 struct DevScene {
   const DevObject* __restrict__ objects;

@@ -234,7 +234,7 @@ typedef struct fs_options {
   int32_t schedule;            /* fs_schedule (AUTO) */
   uint32_t park_lanes;         /* PARKED: park when at most this many lanes still walk (10) */
   uint32_t park_min_tris;      /* meshes whose walks may park (2^19); read at upload */
-  uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (64) */
+  uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (16) */
   uint32_t groups;             /* sample groups per launch; 0 = sized to >= 262144 blocks (0) */
   uint32_t group_major;        /* block order: 0 a tile's groups together (0), 1 group by group */
   uint32_t tile_order;         /* 1 centre-first dispatch of owned tiles (1), 0 index order */

@@ -346,15 +346,20 @@ def test_full_size_properties(scene_dir, gpu_renderer):
 def test_sample_groups_bit_exact(scene_dir, gpu_renderer):
     """A launch of G sample groups (G x 64 spp, folded in sample order by
     fold_groups) gives the frame of G consecutive 64-spp launches, for any G,
-    with a ragged last chunk, on a tile shard, and matches the oracle."""
+    with a ragged last chunk, on a tile shard, and matches the oracle; so do
+    the default 16-sample blocks."""
     r = gpu_renderer
     s = load_scene("c2", scene_dir)
     cam = s.camera(0)
     r.upload(s)
     W, H, spp = 160, 72, 5 * 64 + 7  # 3x2 tiles of 64x64; 5 full 64-spp chunks + a ragged one
     frames = {}
-    for g in ("1", "2", "auto", "2-group-major"):
-        r.set_options(groups=0 if g == "auto" else int(g[0]), group_major=int(g.endswith("major")))
+    for g in ("1", "2", "auto", "2-group-major", "default"):
+        if g == "default":  # 16-sample blocks, all 20 full chunks in one launch, then the 7-spp chunk
+            r.set_options(**fsamd.options_dict(fsamd.options()))
+        else:
+            r.set_options(samples_per_block=64, groups=0 if g == "auto" else int(g[0]),
+                          group_major=int(g.endswith("major")))
         for shard in ((0, 1), (1, 3)):
             f = r.frame(W, H)
             r.render(cam, f, spp=spp, tile_offset=shard[0], tile_stride=shard[1])
@@ -363,6 +368,7 @@ def test_sample_groups_bit_exact(scene_dir, gpu_renderer):
     assert frames["1", (0, 1)][1] == (6, 64)
     assert frames["2", (0, 1)][1] == (4, 128)    # groups 2+2+1, then the 7-spp chunk
     assert frames["auto", (0, 1)][1] == (2, 320)  # a small frame takes all full chunks at once
+    assert frames["default", (0, 1)][1] == (2, 320)
     for key, (planes, _) in frames.items():
         base = frames["1", key[1]][0]
         for p in range(6):
@@ -551,7 +557,7 @@ OPTION_VARIANTS = [
     {"schedule": "lean"},
     {"schedule": "parked", "park_min_tris": 1},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63},
-    {"samples_per_block": 16},
+    {"samples_per_block": 64},
     {"samples_per_block": 7},
     {"xcd_bands": 0},
     {"xcd_bands": 1},
