@@ -48,7 +48,8 @@ WORKLOADS = {
 # Algorithmic bytes per unit of work, from the device SoA record
 # sizes: BVH node 64 B and triangle 64 B (fs_scene.h DevTri), both per lane;
 # an object record 128 B per WAVE (the object loop reads records with scalar
-# loads at a wave-uniform index: one load serves the 64 lanes); per segment
+# loads at a wave-uniform index: one load serves the 64 lanes), and so are
+# the 64-B triangle records of small meshes (fs_options.small_mesh_tris); per segment
 # one material record (76 B) + one normal-table entry (16 B); per sample 12 B
 # of radiance.
 S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
@@ -150,8 +151,8 @@ def main():
     r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
     c = r.counters()
     cf.close()
-    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * c["tri_tests"] + S_OBJ * c["object_loads"]
-                        + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
+    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * (c["tri_tests"] + c["small_tri_loads"])
+                        + S_OBJ * c["object_loads"] + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
     avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
     owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
     per_launch_bytes = bytes_per_sample * owned_samples / launches
@@ -177,6 +178,7 @@ def main():
                 "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),
                 "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2),
                 "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
+                "small_tri_loads_per_sample": round(c["small_tri_loads"] / max(c["samples"], 1), 3),
                 "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
 
     cpu = None

@@ -235,9 +235,7 @@ struct TriData {
   uint32_t axis, face;
   f4 pl;
 };
-__device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
-  const float4* q = reinterpret_cast<const float4*>(T + i);
-  float4 a = q[0], b = q[1], c = q[2], d = q[3];
+__device__ __forceinline__ TriData unpack_tri(float4 a, float4 b, float4 c, float4 d) {
   TriData t;
   t.pl = mk4(a.x, a.y, a.z, a.w);
   t.p1a = b.x;
@@ -254,6 +252,18 @@ __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32
   t.d11 = d.z;
   t.inv = d.w;
   return t;
+}
+__device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
+  const float4* q = reinterpret_cast<const float4*>(T + i);
+  return unpack_tri(q[0], q[1], q[2], q[3]);
+}
+// A triangle at a wave-uniform index (small meshes): read through the
+// constant address space, so the backend uses scalar loads into SGPRs.
+typedef const __attribute__((address_space(4))) float* ConstF;
+__device__ __forceinline__ TriData load_tri_uniform(const DevTri* T, uint32_t i) {
+  ConstF f = (ConstF)(T + i);
+  return unpack_tri(make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]),
+                    make_float4(f[8], f[9], f[10], f[11]), make_float4(f[12], f[13], f[14], f[15]));
 }
 __device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint32_t i) {
   return T[i].face_axis & 0x3FFFFFFFu;
@@ -298,6 +308,7 @@ __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32
   t.pl = mk4(e.x, e.y, e.z, e.w);
   return t;
 }
+__device__ __forceinline__ TriData load_tri_uniform(const DevTri* T, uint32_t i) { return load_tri(T, i); }
 __device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint32_t i) { return T[i].face; }
 // intersect.cpp:146-177 with the triangle-only terms precomputed: vp is
 // planar-mapped like v0/v1 and the reference's dot products follow.
@@ -347,6 +358,7 @@ template <bool COUNT>
 struct Tally {
   uint32_t nodes = 0, tris = 0, prims = 0;
   uint32_t objs = 0;  // object records read (wave-uniform loads: counted once per wave)
+  uint32_t utris = 0;  // small-mesh triangle records read (wave-uniform loads: once per wave)
 #ifdef FS_PHASE_PROF
   // wave-level loop trips, counted by the first active lane of each trip
   uint32_t node_trips = 0, leaf_trips = 0, lane_nodes = 0, lane_leaves = 0;
@@ -603,6 +615,33 @@ struct WalkSuspend {
 // parked leaves together. Inner-node and triangle code no longer interleave
 // per iteration. The closest hit is a total order on (t, face), so the test
 // order does not change the result.
+// One face of mesh object oi against the ray: the reference test
+// (intersect.cpp:357-419, or the point test of a zero-length ray) and the
+// closest-hit update, lower face index first among equal t.
+__device__ __forceinline__ void tri_candidate(const DevScene& S, const TriData& T, uint32_t ti, int32_t oi,
+                                              const Ray& r, bool zl, MinHit& h) {
+  float t, u, v;
+  bool hit;
+  if (!zl) {
+    f3 p;
+    hit = ray_tri(T, r, t, p, u, v);
+  } else {
+    hit = point_in_tri(T, r.start, u, v);
+    t = 0.0f;
+  }
+  if (hit) {
+    bool better = t < h.t || (t == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
+    if (better) {
+      h.t = t;
+      h.obj = oi;
+      h.prim = ti;
+      h.u = u;
+      h.v = v;
+      h.point = zl ? 1u : 0u;
+    }
+  }
+}
+
 template <bool COUNT, int ZLMODE = -1>  // ZLMODE: 0/1 = ray known (non-)zero-length, -1 = runtime zl
 __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl_rt, MinHit& h,
                                           Tally<COUNT>& tally) {
@@ -612,26 +651,23 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
     uint32_t ti = first + i;
     TriData T = load_tri(S.tris, ti);
     if (COUNT) tally.tris++;
-    float t, u, v;
-    bool hit;
-    if (!zl) {
-      f3 p;
-      hit = ray_tri(T, r, t, p, u, v);
-    } else {
-      hit = point_in_tri(T, r.start, u, v);
-      t = 0.0f;
-    }
-    if (hit) {
-      bool better = t < h.t || (t == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
-      if (better) {
-        h.t = t;
-        h.obj = oi;
-        h.prim = ti;
-        h.u = u;
-        h.v = v;
-        h.point = zl ? 1u : 0u;
-      }
-    }
+    tri_candidate(S, T, ti, oi, r, zl, h);
+  }
+}
+
+// A small mesh (DevObject::i3 = n faces from triangle `first`): every face
+// at a wave-uniform index, no BVH walk. The walk's culling is conservative
+// and the closest hit is a total order on (t, face), so testing all faces
+// gives the walk's hit bit for bit; the faces come in SGPRs, not as
+// dependent per-lane node and triangle fetches.
+template <bool COUNT>
+__device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
+                                                 const Ray& r, bool zl, MinHit& h, Tally<COUNT>& tally) {
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t ti = first + i;
+    TriData T = load_tri_uniform(S.tris, ti);
+    if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.utris++;
+    tri_candidate(S, T, ti, oi, r, zl, h);
   }
 }
 
@@ -831,7 +867,10 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
   if (kind == FS_OBJ_MESH) {
     if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) return false;
     const int32_t before = h.obj;
-    traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+    if (o->i3)
+      small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
+    else
+      traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
     const bool wrote = h.obj == (int32_t)oi && before != (int32_t)oi;
     if (TEX && wrote && o->i4) h.tc = (int32_t)oi;  // mesh.cpp:300-311: only with texcoords
     return wrote;
@@ -1036,7 +1075,10 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
       bool visit = resume_here || ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
       uint64_t t1 = FS_TICK();
-      if (SUSP) {
+      if (o->i3) {  // a small mesh: its faces, no walk (never parks)
+        if (visit)
+          small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
+      } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
         if (visit)
@@ -1625,6 +1667,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
     atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
     atomicAdd(&counters->object_loads, (unsigned long long)tally.objs);
+    atomicAdd(&counters->small_tri_loads, (unsigned long long)tally.utris);
   }
 }
 
@@ -2030,6 +2073,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->bvh_bins < 2 || o->bvh_bins > 64) *why = "bvh_bins must be 2..64";
   else if (o->node_layout > FS_NODE_LAYOUT_PAIRS) *why = "unknown node_layout";
   else if (o->persist > 1) *why = "persist must be 0 or 1";
+  else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
   else return true;
   return false;
 }
@@ -2109,6 +2153,7 @@ int fs_options_default(fs_options* o) {
   o->node_layout = FS_NODE_LAYOUT_DEPTH_FIRST;
   o->build_log = 0;
   o->persist = 1;
+  o->small_mesh_tris = 16;
   return FS_OK;
 }
 
@@ -2478,6 +2523,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->tri_tests = c.tri_tests;
   out->prim_tests = c.prim_tests;
   out->object_loads = c.object_loads;
+  out->small_tri_loads = c.small_tri_loads;
 #ifdef FS_PHASE_PROF
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "

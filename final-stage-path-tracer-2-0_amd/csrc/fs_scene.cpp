@@ -785,6 +785,7 @@ BuildOptions BuildOptions::from(const fs_options* o) {
   b.threads = o->bvh_threads;
   b.pair_layout = o->node_layout == FS_NODE_LAYOUT_PAIRS;
   b.park_min_tris = o->park_min_tris;
+  b.small_mesh_tris = o->small_mesh_tris <= kMaxSmallMeshTris ? o->small_mesh_tris : def.small_mesh_tris;
   b.log = o->build_log != 0;
   return b;
 }
@@ -856,6 +857,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   // Meshes: MeshObject::MeshObject + BuildBvh face planes.
   struct MeshOut {
     uint32_t root = 0;
+    uint32_t first_tri = 0, small = 0;  // a small mesh's triangle slots (host build)
     bool tree = false;
     bool normals = false;
     bool texcoords = false;
@@ -1028,6 +1030,8 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       S.nodes.push_back(blank);
     }
     const uint32_t node_begin = (uint32_t)S.nodes.size();
+    mesh_out[mi].first_tri = (uint32_t)S.tris.size();  // the builder appends the mesh's faces in leaf order
+    if (m.num_triangles <= opt.small_mesh_tris) mesh_out[mi].small = m.num_triangles;
     BvhBuilder builder(&S.nodes, &S.tris, &S.tri_normals, &S.tri_tex, &mtris, &mnormals, &mtex, opt);
     auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
@@ -1081,7 +1085,8 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i0 = (int32_t)mo.root;
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
-      D.i3 = 0;
+      D.i3 = (int32_t)mo.small;
+      if (mo.small) std::memcpy(&D.d[6], &mo.first_tri, 4);
       D.i4 = mo.texcoords ? 1 : 0;
       D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);

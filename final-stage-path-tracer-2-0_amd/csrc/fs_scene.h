@@ -26,7 +26,8 @@ struct DevObject {
   int32_t i0;    // MESH: BVH root node index
   int32_t i1;    // MESH: 1 if the mesh has vertex normals
   int32_t i2;    // MESH: 1 if the reference would have built a tree (mesh.cpp:119)
-  int32_t i3;    // unused (0)
+  int32_t i3;    // MESH: n > 0 for a small mesh of n triangles (fs_options.small_mesh_tris),
+                 // tested face by face from triangle d[6] (bits) on, without a walk
   int32_t i4;    // MESH: 1 if the mesh has texcoords (mesh.cpp:300)
   int32_t i5;    // MESH: 1 if its walks may park (>= kParkMinTris triangles, SUSP schedule)
   float d[40];
@@ -37,7 +38,8 @@ struct DevObject {
   //         of the 8 corners (a conservative cull, not a reference test)
   // QUAD    d0-3 plane, d4-6 origin, d7 half width, d8 half height,
   //         d9-11 bitangent, d12-14 tangent
-  // MESH    d0-5 reference root bounds (min, max) — mesh.cpp:129-133
+  // MESH    d0-5 reference root bounds (min, max) — mesh.cpp:129-133;
+  //         d6 (uint bits) first triangle of a small mesh
 };
 static_assert(sizeof(DevObject) == 192, "DevObject layout");
 
@@ -56,6 +58,7 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kMaxLeafCount = 127;
 constexpr uint32_t kMaxTriangles = 1u << 24;
 constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
+constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
 // Triangle record: the operands of the reference test (intersect.cpp:357-419)
 // with every ray-independent term precomputed on the host by the same float
@@ -156,6 +159,7 @@ struct BuildOptions {
   uint32_t threads = 0;         // host build threads, 0 = 16
   bool pair_layout = false;     // sibling-pair node layout (host build)
   uint32_t park_min_tris = kParkMinTris;
+  uint32_t small_mesh_tris = 16;  // meshes tested face by face (DevObject::i3)
   bool log = false;             // build phases to stderr
   static BuildOptions from(const fs_options* o);  // NULL: the defaults
 };

@@ -87,7 +87,8 @@ class fs_render_params(C.Structure):
 
 class fs_counters(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("prim_tests", C.c_uint64), ("object_loads", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("prim_tests", C.c_uint64), ("object_loads", C.c_uint64),
+                ("small_tri_loads", C.c_uint64)]
 
 
 class fs_options(C.Structure):
@@ -96,7 +97,7 @@ class fs_options(C.Structure):
                 ("tile_order", C.c_uint32), ("xcd_bands", C.c_uint32), ("gpu_bvh_min_tris", C.c_uint32),
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
-                ("persist", C.c_uint32)]
+                ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH

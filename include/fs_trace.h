@@ -209,6 +209,9 @@ typedef struct fs_counters {
   uint64_t prim_tests;  /* analytic object tests (per lane) */
   uint64_t object_loads; /* object records read: wave-uniform scalar loads, one per
                             wave per object visit of a closest-hit query */
+  uint64_t small_tri_loads; /* triangle records of small meshes (fs_options.small_mesh_tris),
+                               wave-uniform loads, once per wave; their per-lane tests are
+                               not in tri_tests */
 } fs_counters;
 
 typedef struct fs_context fs_context;
@@ -248,6 +251,9 @@ typedef struct fs_options {
   uint32_t build_log;          /* 1: scene build phases to stderr (0) */
   uint32_t persist;            /* 1 persistent waves pulling blocks from per-XCD queues (1),
                                   0 one wave per block */
+  uint32_t small_mesh_tris;    /* host-built meshes of at most this many triangles are tested
+                                  face by face with wave-uniform loads, no BVH walk (16; 0 off,
+                                  max 64); read at upload */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */

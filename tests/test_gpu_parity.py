@@ -568,6 +568,8 @@ OPTION_VARIANTS = [
     {"bvh_threads": 1},
     {"persist": 0},
     {"persist": 0, "samples_per_block": 7, "groups": 3},
+    {"small_mesh_tris": 0},
+    {"small_mesh_tris": 64},
 ]
 
 

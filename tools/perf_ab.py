@@ -13,6 +13,10 @@ import fsamd  # noqa: E402
 import scenes  # noqa: E402
 
 
+BUILD_FIELDS = {"park_min_tris", "gpu_bvh_min_tris", "bvh_leaf", "bvh_bins", "bvh_threads", "node_layout",
+                "small_mesh_tris"}
+
+
 def main():
     variants = sys.argv[1].split(",")
     names = sys.argv[2].split(",")
@@ -27,13 +31,19 @@ def main():
         fsamd.initialize_materials()
         r = fsamd.Renderer(0)
         r.upload(s)
+        uploaded = tuple(fsamd.options_dict(fsamd.options())[k] for k in sorted(BUILD_FIELDS))
         cam = s.camera(0)
         f = r.frame(W, H)
         res = {v: [] for v in variants}
         ref = None
         for rd in range(rounds + 1):
             for v in variants:
-                r.set_options(**fsamd.options_dict(fsamd.options(**fsamd.parse_variant(v))))
+                od = fsamd.options_dict(fsamd.options(**fsamd.parse_variant(v)))
+                r.set_options(**od)
+                build = tuple(od[k] for k in sorted(BUILD_FIELDS))
+                if build != uploaded:  # scene-build fields are read at upload
+                    r.upload(s)
+                    uploaded = build
                 f.reset()
                 r.render(cam, f, spp=spp)
                 ms = r.last_render_ms()
