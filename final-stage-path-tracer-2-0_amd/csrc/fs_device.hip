@@ -1085,6 +1085,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
           park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
                                           o->i5 ? susp_thr : 0u, live, slp);
         if (resume_here) resuming = false;
+#ifdef FS_PHASE_PROF
+        if (park) {
+          pa.cull += t1 - t0;
+          pa.trav += FS_TICK() - t1;
+        }
+#endif
         if (park) continue;
       } else if (visit) {
         traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
@@ -1535,6 +1541,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
+      FS_PHASE(2);
       {  // histogram of node visits per traced segment: 0,1-4,5-8,9-16,17-32,33-64,65-128,>128
         uint32_t nv = tally.lane_nodes - nodes_before, bin = 0;
         if (nv > 0) bin = 1;
@@ -1558,6 +1565,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           atomicAdd(&counters->phase[25], (unsigned long long)red[1]);
         }
       }
+      tk = __builtin_readcyclecounter();  // the histogram's own time is left out
 #else
       PhaseAcc pa;
       scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);

@@ -209,6 +209,311 @@ bool decompress_rle(uint8_t* dst, size_t dst_len, const uint8_t* src, size_t src
 
 int type_size(int t) { return t == kHalf ? 2 : 4; }
 
+// ---- PIZ: tinyexr's DecompressPiz (tiny_exr_loader.h:9303-9415), the
+// OpenEXR PIZ scheme: a bitmap of the 16-bit values that occur and its
+// reverse lookup table (:9155-9173), a canonical Huffman code with run
+// lengths (:8201-9110), and a 2D Haar wavelet per channel layer
+// (:7909-8187). Restated from those routines; the Huffman decoder keeps
+// their table layout (14-bit primary table, long codes listed per entry)
+// and their error points, and, as tinyexr does, the decoder's failures
+// are not fatal: the buffer keeps what was decoded (DecompressPiz only
+// fails on a bad bitmap range).
+namespace piz {
+constexpr int kEncSize = (1 << 16) + 1;  // HUF_ENCSIZE
+constexpr int kDecBits = 14, kDecSize = 1 << kDecBits, kDecMask = kDecSize - 1;
+constexpr int kShortZeroRun = 59, kLongZeroRun = 63;
+constexpr int kShortestLongRun = 2 + kLongZeroRun - kShortZeroRun;
+constexpr int kBitmapSize = (1 << 16) >> 3;
+
+struct Bits {  // MSB-first bit reader over [p, end); reads past the end give zero bytes
+  const uint8_t* p;
+  const uint8_t* end;
+  uint64_t c = 0;
+  int lc = 0;
+  void byte() {
+    c = (c << 8) | (p < end ? *p : 0u);
+    p++;
+    lc += 8;
+  }
+  uint64_t take(int n) {  // getBits
+    while (lc < n) byte();
+    lc -= n;
+    return (c >> lc) & ((1ull << n) - 1);
+  }
+};
+
+// hufUnpackEncTable + hufCanonicalCodeTable: code lengths for [im, iM] with
+// zero runs, then canonical codes (hcode = length | code << 6).
+bool unpack_table(Bits& b, const uint8_t* start, long ni, int im, int iM, std::vector<uint64_t>& hcode) {
+  std::fill(hcode.begin(), hcode.end(), 0);
+  for (; im <= iM; im++) {
+    if (b.p - start > ni) return false;
+    uint64_t l = hcode[im] = b.take(6);
+    if (l == (uint64_t)kLongZeroRun) {
+      if (b.p - start > ni) return false;
+      int zerun = (int)b.take(8) + kShortestLongRun;
+      if (im + zerun > iM + 1) return false;
+      while (zerun--) hcode[im++] = 0;
+      im--;
+    } else if (l >= (uint64_t)kShortZeroRun) {
+      int zerun = (int)l - kShortZeroRun + 2;
+      if (im + zerun > iM + 1) return false;
+      while (zerun--) hcode[im++] = 0;
+      im--;
+    }
+  }
+  uint64_t n[59] = {0};
+  for (int i = 0; i < kEncSize; i++) n[hcode[i]]++;  // lengths are < 59 here
+  uint64_t c = 0;
+  for (int l = 58; l > 0; l--) {  // lowest code of each length, longest first
+    uint64_t nc = (c + n[l]) >> 1;
+    n[l] = c;
+    c = nc;
+  }
+  for (int i = 0; i < kEncSize; i++) {
+    uint64_t l = hcode[i];
+    if (l > 0) hcode[i] = l | (n[l]++ << 6);
+  }
+  return true;
+}
+
+struct DecEntry {
+  int len = 0;            // short code: its length
+  int lit = 0;            // short code: the symbol
+  std::vector<int> longs; // symbols of the long codes whose top 14 bits index this entry
+};
+
+// hufBuildDecTable
+bool build_dec(const std::vector<uint64_t>& hcode, int im, int iM, std::vector<DecEntry>& dec) {
+  for (; im <= iM; im++) {
+    const uint64_t c = hcode[im] >> 6;
+    const int l = (int)(hcode[im] & 63);
+    if (c >> l) return false;
+    if (l > kDecBits) {
+      DecEntry& e = dec[c >> (l - kDecBits)];
+      if (e.len) return false;
+      e.longs.push_back(im);
+    } else if (l) {
+      const uint64_t first = c << (kDecBits - l);
+      for (uint64_t i = 0; i < (1ull << (kDecBits - l)); i++) {
+        DecEntry& e = dec[first + i];
+        if (e.len || !e.longs.empty()) return false;
+        e.len = l;
+        e.lit = im;
+      }
+    }
+  }
+  return true;
+}
+
+// getCode: a symbol, or (the run-length pseudo-symbol rlc) an 8-bit count of
+// repeats of the previous output value.
+bool emit(int sym, int rlc, Bits& b, const uint8_t* in_end, uint16_t*& out, const uint16_t* ob, const uint16_t* oe) {
+  if (sym == rlc) {
+    if (b.lc < 8) {
+      if (b.p + 1 >= in_end) return false;
+      b.byte();
+    }
+    b.lc -= 8;
+    uint8_t cs = (uint8_t)(b.c >> b.lc);
+    if (out + cs > oe) return false;
+    if (out - 1 <= ob) return false;  // (tinyexr: a run needs two earlier values)
+    const uint16_t v = out[-1];
+    while (cs-- > 0) *out++ = v;
+  } else if (out < oe) {
+    *out++ = (uint16_t)sym;
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// hufDecode over ni bits
+bool decode(const std::vector<uint64_t>& hcode, const std::vector<DecEntry>& dec, const uint8_t* in, long ni, int rlc,
+            uint16_t* out, size_t no) {
+  Bits b{in, in + (ni + 7) / 8};
+  const uint8_t* ie = b.end;
+  uint16_t* const ob = out;
+  const uint16_t* oe = out + no;
+  while (b.p < ie) {
+    b.byte();
+    while (b.lc >= kDecBits) {
+      const DecEntry& e = dec[(b.c >> (b.lc - kDecBits)) & kDecMask];
+      if (e.len) {
+        b.lc -= e.len;
+        if (!emit(e.lit, rlc, b, ie, out, ob, oe)) return false;
+      } else {
+        if (e.longs.empty()) return false;
+        size_t j = 0;
+        for (; j < e.longs.size(); j++) {
+          const int l = (int)(hcode[e.longs[j]] & 63);
+          while (b.lc < l && b.p < ie) b.byte();
+          if (b.lc >= l && (hcode[e.longs[j]] >> 6) == ((b.c >> (b.lc - l)) & ((1ull << l) - 1))) {
+            b.lc -= l;
+            if (!emit(e.longs[j], rlc, b, ie, out, ob, oe)) return false;
+            break;
+          }
+        }
+        if (j == e.longs.size()) return false;
+      }
+    }
+  }
+  const int i = (int)((8 - ni) & 7);  // the padding bits of the last byte
+  b.c >>= i;
+  b.lc -= i;
+  while (b.lc > 0) {
+    const DecEntry& e = dec[(b.c << (kDecBits - b.lc)) & kDecMask];
+    if (!e.len) return false;
+    b.lc -= e.len;
+    if (!emit(e.lit, rlc, b, ie, out, ob, oe)) return false;
+  }
+  return (size_t)(out - ob) == no;
+}
+
+// hufUncompress; its callers ignore the result, and so do we.
+void huf_uncompress(const uint8_t* comp, long n_comp, std::vector<uint16_t>& raw) {
+  if (n_comp < 20) return;
+  const int im = (int)rd<uint32_t>(comp), iM = (int)rd<uint32_t>(comp + 4);
+  const int n_bits = (int)rd<uint32_t>(comp + 12);
+  if (im < 0 || im >= kEncSize || iM < 0 || iM >= kEncSize) return;
+  std::vector<uint64_t> hcode(kEncSize);
+  Bits b{comp + 20, comp + n_comp};
+  // (a table that fails to unpack leaves the data pointer at the table)
+  const uint8_t* data = unpack_table(b, comp + 20, n_comp - 20, im, iM, hcode) ? b.p : comp + 20;
+  if (n_bits < 0 || (long)n_bits > 8 * (n_comp - (long)(data - comp))) return;
+  std::vector<DecEntry> dec(kDecSize);
+  build_dec(hcode, im, iM, dec);
+  decode(hcode, dec, data, n_bits, iM, raw.data(), raw.size());
+}
+
+// wdec14 / wdec16: one inverse Haar step (14-bit without, 16-bit with modulo
+// arithmetic)
+inline void wdec14(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+  const int hi = (int16_t)h;
+  const int ai = (int16_t)l + (hi & 1) + (hi >> 1);
+  a = (uint16_t)(int16_t)ai;
+  b = (uint16_t)(int16_t)(ai - hi);
+}
+inline void wdec16(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+  const int m = l, d = h;
+  const int bb = (m - (d >> 1)) & 0xFFFF;
+  const int aa = (d + bb - (1 << 15)) & 0xFFFF;
+  b = (uint16_t)bb;
+  a = (uint16_t)aa;
+}
+
+// wav2Decode: the 2D inverse transform of one layer (nx x ny values at
+// strides ox, oy), coarsest level first.
+void wav2_decode(uint16_t* in, int nx, int ox, int ny, int oy, uint16_t mx) {
+  const bool w14 = mx < (1 << 14);
+  auto dec = [w14](uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
+    if (w14)
+      wdec14(l, h, a, b);
+    else
+      wdec16(l, h, a, b);
+  };
+  const int n = nx > ny ? ny : nx;
+  int p = 1;
+  while (p <= n) p <<= 1;
+  p >>= 1;
+  int p2 = p;
+  p >>= 1;
+  while (p >= 1) {
+    uint16_t* py = in;
+    uint16_t* const ey = in + (ptrdiff_t)oy * (ny - p2);
+    const int oy1 = oy * p, oy2 = oy * p2, ox1 = ox * p, ox2 = ox * p2;
+    uint16_t i00, i01, i10, i11;
+    for (; py <= ey; py += oy2) {
+      uint16_t* px = py;
+      uint16_t* const ex = py + (ptrdiff_t)ox * (nx - p2);
+      for (; px <= ex; px += ox2) {
+        uint16_t* p01 = px + ox1;
+        uint16_t* p10 = px + oy1;
+        uint16_t* p11 = p10 + ox1;
+        dec(*px, *p10, i00, i10);
+        dec(*p01, *p11, i01, i11);
+        dec(i00, i01, *px, *p01);
+        dec(i10, i11, *p10, *p11);
+      }
+      if (nx & p) {  // odd column
+        uint16_t* p10 = px + oy1;
+        dec(*px, *p10, i00, *p10);
+        *px = i00;
+      }
+    }
+    if (ny & p) {  // odd line
+      uint16_t* px = py;
+      uint16_t* const ex = py + (ptrdiff_t)ox * (nx - p2);
+      for (; px <= ex; px += ox2) {
+        uint16_t* p01 = px + ox1;
+        dec(*px, *p01, i00, *p01);
+        *px = i00;
+      }
+    }
+    p2 = p;
+    p >>= 1;
+  }
+}
+}  // namespace piz
+
+// DecompressPiz: dst_len bytes of `num_lines` lines of `width` pixels, the
+// channels planar per line as the other codecs produce them.
+bool decompress_piz(uint8_t* dst, size_t dst_len, const uint8_t* src, size_t src_len, const std::vector<Channel>& chans,
+                    int width, int num_lines) {
+  if (src_len == dst_len) {  // stored uncompressed (tinyexr issue 40)
+    std::memcpy(dst, src, src_len);
+    return true;
+  }
+  if (src_len < 4) return false;
+  const uint16_t min_nz = rd<uint16_t>(src), max_nz = rd<uint16_t>(src + 2);
+  const uint8_t* ptr = src + 4;
+  if (max_nz >= piz::kBitmapSize) return false;
+  std::vector<uint8_t> bitmap(piz::kBitmapSize, 0);
+  if (min_nz <= max_nz) {
+    const size_t n = (size_t)(max_nz - min_nz + 1);
+    if ((size_t)(ptr - src) + n > src_len) return false;
+    std::memcpy(bitmap.data() + min_nz, ptr, n);
+    ptr += n;
+  }
+  // reverseLutFromBitmap: lut[k] = the k-th value present (0 always is)
+  std::vector<uint16_t> lut(1 << 16, 0);
+  int k = 0;
+  for (int i = 0; i < (1 << 16); i++)
+    if (i == 0 || (bitmap[i >> 3] & (1 << (i & 7)))) lut[k++] = (uint16_t)i;
+  const uint16_t max_value = (uint16_t)(k - 1);
+  if ((size_t)(ptr - src) + 4 > src_len) return false;
+  const int32_t length = rd<int32_t>(ptr);
+  ptr += 4;
+  // tinyexr sizes the 16-bit buffer in bytes (twice the values it holds);
+  // the Huffman stream fills the first half.
+  std::vector<uint16_t> tmp(dst_len, 0);
+  const long avail = (long)(src_len - (size_t)(ptr - src));
+  piz::huf_uncompress(ptr, std::min<long>(length, avail), tmp);
+  // per channel: size/2 interleaved 16-bit layers of nx x ny values
+  uint16_t* at = tmp.data();
+  std::vector<uint16_t*> starts(chans.size());
+  std::vector<int> layers(chans.size());
+  for (size_t c = 0; c < chans.size(); c++) {
+    layers[c] = type_size(chans[c].pixel_type) / 2;
+    starts[c] = at;
+    at += (size_t)width * num_lines * layers[c];
+  }
+  for (size_t c = 0; c < chans.size(); c++)
+    for (int j = 0; j < layers[c]; j++)
+      piz::wav2_decode(starts[c] + j, width, layers[c], num_lines, width * layers[c], max_value);
+  for (uint16_t& v : tmp) v = lut[v];  // applyLut over the whole buffer
+  uint8_t* out = dst;
+  std::vector<uint16_t*> cur(starts);
+  for (int y = 0; y < num_lines; y++)
+    for (size_t c = 0; c < chans.size(); c++) {
+      const size_t n = (size_t)width * layers[c];
+      std::memcpy(out, cur[c], n * 2);
+      out += n * 2;
+      cur[c] += n;
+    }
+  return true;
+}
+
 // DecodePixelData: one block of `num_lines` lines, `width` pixels, into the
 // per-channel float planes (HALF converted; UINT bits kept, as LoadEXR later
 // reads every plane as float). Rows follow tinyexr's line_order handling.
@@ -229,6 +534,8 @@ bool decode_block(const Header& h, std::vector<std::vector<float>>& planes, cons
     if (!decompress_zip(raw.data(), raw_len, data, data_len)) return false;
   } else if (h.compression == kRle) {
     if (!decompress_rle(raw.data(), raw_len, data, data_len)) return false;
+  } else if (h.compression == kPiz) {
+    if (!decompress_piz(raw.data(), raw_len, data, data_len, h.channels, width, num_lines)) return false;
   } else {
     return false;
   }
@@ -299,9 +606,7 @@ int parse_header(const uint8_t* p, size_t size, size_t* pos, Header* h, const ch
   }
   if (!has_channels || !has_compression || !has_dw)
     return exr_fail(err, kInvalidHeader, "Required attribute (channels/compression/dataWindow) missing.");
-  if (h->compression == kPiz)
-    return exr_fail(err, kUnsupportedFeature, "PIZ compression is not supported by this loader.");
-  if (h->compression > kZip) return exr_fail(err, kUnsupportedFormat, "Unsupported compression type.");
+  if (h->compression > kPiz) return exr_fail(err, kUnsupportedFormat, "Unsupported compression type.");
   for (const Channel& c : h->channels)
     if (c.pixel_type != kUint && c.pixel_type != kHalf && c.pixel_type != kFloat)
       return exr_fail(err, kInvalidHeader, "Invalid pixel type.");
@@ -350,7 +655,7 @@ int LoadEXR(float** out_rgba, int* width, int* height, const char* filename, con
   bool alpha_only = iA == 0 && iR < 0 && iG < 0 && iB < 0;
   std::vector<float> rgba((size_t)4 * dw * dh);
   if (!h.tiled) {
-    int lines = h.compression == kZip ? 16 : 1;
+    int lines = h.compression == kZip ? 16 : h.compression == kPiz ? 32 : 1;  // num_scanline_blocks
     int nblocks = dh / lines + (dh % lines ? 1 : 0);
     if (pos + 8ull * nblocks > size) return exr_fail(err, kInvalidData, "Insufficient data size in offset table.");
     std::vector<std::vector<float>> planes(nch, std::vector<float>((size_t)dw * dh, 0.0f));

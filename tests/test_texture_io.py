@@ -132,6 +132,80 @@ def test_exr_tiled(tmp_path, comp):
     np.testing.assert_array_equal(out[..., :3], np.stack([r, g, b], -1))
 
 
+def _piz_channels(H, W, seed, noisy):
+    """A (UINT bits), B (smooth HALF), G (few HALF values), R (FLOAT; noisy:
+    thousands of distinct 16-bit words, so the modulo 16-bit wavelet)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W]
+    b = (0.5 + 0.25 * np.sin(xx / 7.0) * np.cos(yy / 5.0)).astype(np.float32)
+    g = (rng.integers(0, 40, (H, W)) / 8.0).astype(np.float32)
+    if noisy:
+        r = (rng.standard_normal((H, W)) * 3.0).astype(np.float32)
+        a = rng.integers(0, 1 << 20, (H, W)).astype(np.uint32)
+    else:
+        r = (xx % 5 + yy // 3).astype(np.float32)  # small integers: the low 16-bit words are zero
+        a = (xx // 3 + 100 * (yy // 4)).astype(np.uint32)
+    return a, b, g, r
+
+
+@pytest.mark.parametrize("tiles", [None, (16, 8), (32, 32)])
+def test_exr_piz(tmp_path, tiles):
+    """PIZ (tinyexr DecompressPiz, tiny_exr_loader.h:9303-9415): bitmap +
+    reverse lookup table, Huffman with run lengths, 2D Haar wavelet on each
+    16-bit layer (a FLOAT or UINT channel is two interleaved layers), 32-line
+    scanline blocks (the last one ragged) or ragged tiles. The file comes
+    from an independent encoder (tests/exrwrite.py), so the pixels are known."""
+    H, W = 70, 45
+    a, b, g, r = _piz_channels(H, W, 5, noisy=tiles is None)
+    p = tmp_path / "piz.exr"
+    X.write(p, [("A", X.UINT, a), ("B", X.HALF, b), ("G", X.HALF, g), ("R", X.FLOAT, r)], compression=X.PIZ,
+            tiles=tiles)
+    q = tmp_path / "none.exr"
+    X.write(q, [("A", X.UINT, a), ("B", X.HALF, b), ("G", X.HALF, g), ("R", X.FLOAT, r)], tiles=tiles)
+    if tiles != (16, 8):  # (16x8 tiles: the value bitmap outweighs 1.5 KB tiles, so they are stored raw)
+        assert p.stat().st_size < q.stat().st_size  # compressed blocks, not stored ones
+    out = fsamd.load_exr(p)
+    np.testing.assert_array_equal(out[..., 0], r)
+    np.testing.assert_array_equal(out[..., 1], g.astype(np.float16).astype(np.float32))
+    np.testing.assert_array_equal(out[..., 2], b.astype(np.float16).astype(np.float32))
+    np.testing.assert_array_equal(out[..., 3].view(np.uint32), a)  # UINT bits kept
+    np.testing.assert_array_equal(out, fsamd.load_exr(q))
+
+
+def test_exr_piz_small_and_stored_blocks(tmp_path):
+    """Blocks whose PIZ form is not smaller are stored raw (tinyexr issue 40:
+    equal sizes mean uncompressed); 1-pixel-wide and 1-line images take the
+    wavelet's odd-column / odd-line paths only."""
+    rng = np.random.default_rng(9)
+    for H, W in ((1, 1), (1, 7), (9, 1), (3, 2)):
+        r = rng.standard_normal((H, W)).astype(np.float32)
+        p = tmp_path / f"s{H}x{W}.exr"
+        X.write(p, [("B", X.FLOAT, r), ("G", X.FLOAT, r), ("R", X.FLOAT, r)], compression=X.PIZ)
+        out = fsamd.load_exr(p)
+        for c in range(3):
+            np.testing.assert_array_equal(out[..., c], r)
+    H, W = 32, 700  # > 16384 distinct 16-bit words in one block: the modulo (16-bit) wavelet
+    yy, xx = np.mgrid[0:H, 0:W]
+    r = (1.0 + 0.5 * np.cos(xx * 0.0091 - yy * 0.17)).astype(np.float32)  # smooth, full-precision mantissas
+    g = (2.0 + np.sin(xx * 0.0137 + yy * 0.31)).astype(np.float32)
+    words = np.concatenate([r.view(np.uint16).ravel(), g.view(np.uint16).ravel()])
+    assert len(np.unique(words)) > 1 << 14
+    p = tmp_path / "w16.exr"
+    X.write(p, [("B", X.FLOAT, g), ("G", X.FLOAT, r), ("R", X.FLOAT, r)], compression=X.PIZ)
+    assert p.stat().st_size < 0.9 * (H * W * 12)  # compressed, not stored
+    out = fsamd.load_exr(p)
+    np.testing.assert_array_equal(out[..., 0], r)
+    np.testing.assert_array_equal(out[..., 2], g)
+    H, W = 64, 33  # one constant channel next to noise: long zero runs after the first symbols
+    r = np.full((H, W), 0.5, np.float32)
+    g = rng.standard_normal((H, W)).astype(np.float32)
+    p = tmp_path / "runs.exr"
+    X.write(p, [("B", X.HALF, r), ("G", X.FLOAT, g), ("R", X.HALF, r)], compression=X.PIZ)
+    out = fsamd.load_exr(p)
+    np.testing.assert_array_equal(out[..., 0], r)
+    np.testing.assert_array_equal(out[..., 1], g)
+
+
 def test_exr_alpha_only_and_errors(tmp_path):
     a = np.arange(12, dtype=np.float32).reshape(3, 4)
     p = tmp_path / "a.exr"
@@ -142,10 +216,6 @@ def test_exr_alpha_only_and_errors(tmp_path):
     p = tmp_path / "rg.exr"
     X.write(p, [("G", X.FLOAT, a), ("R", X.FLOAT, a)])
     with pytest.raises(fsamd.FsError, match="B channel not found"):
-        fsamd.load_exr(p)
-    p = tmp_path / "piz.exr"
-    X.write(p, [("B", X.FLOAT, a), ("G", X.FLOAT, a), ("R", X.FLOAT, a)], compression=X.PIZ)
-    with pytest.raises(fsamd.FsError, match="PIZ"):
         fsamd.load_exr(p)
     with pytest.raises(fsamd.FsError):
         fsamd.load_exr(tmp_path / "missing.exr")
