@@ -643,10 +643,10 @@ __device__ __forceinline__ void tri_candidate(const DevScene& S, const TriData& 
 }
 
 template <bool COUNT, int ZLMODE = -1>  // ZLMODE: 0/1 = ray known (non-)zero-length, -1 = runtime zl
-__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl_rt, MinHit& h,
-                                          Tally<COUNT>& tally) {
+__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t base, uint32_t w, int32_t oi, const Ray& r,
+                                          bool zl_rt, MinHit& h, Tally<COUNT>& tally) {
   const bool zl = ZLMODE < 0 ? zl_rt : ZLMODE == 1;
-  uint32_t cnt = (w >> 24) & 0x7Fu, first = w & 0xFFFFFFu;
+  uint32_t cnt = leaf_count(w), first = base + (w & kLeafFirstMask);  // global triangle slot
   for (uint32_t i = 0; i < cnt; i++) {
     uint32_t ti = first + i;
     TriData T = load_tri(S.tris, ti);
@@ -701,7 +701,8 @@ __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) {
 // moves on and they resume from *ws in a later iteration (same operations in
 // the same order per lane).
 template <bool COUNT, bool SUSP = false, int ZLMODE = -1>  // ZLMODE as in test_leaf
-__device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl_rt,
+__device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, uint32_t base, int32_t oi, const Ray& r,
+                                            bool zl_rt,
                                             MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                             WalkSuspend* ws = nullptr, bool resume = false, uint32_t thr = 0,
                                             uint32_t live = 0, const Slopes* pre = nullptr) {
@@ -782,13 +783,13 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       FS_WAVE_TRIP(tally.leaf_trips);
       tally.lane_leaves++;
 #endif
-      uint32_t cnt = (leaf >> 24) & 0x7Fu;
+      uint32_t cnt = leaf_count(leaf);
       if (cnt) {
-        test_leaf<COUNT, ZLMODE>(S, (leaf & 0x80FFFFFFu) | (1u << 24), oi, r, zl, h, tally);
+        test_leaf<COUNT, ZLMODE>(S, base, leaf_word(1, leaf & kLeafFirstMask), oi, r, zl, h, tally);
         cnt--;
       }
       if (cnt) {
-        leaf = kLeafBit | (cnt << 24) | ((leaf & 0xFFFFFFu) + 1u);
+        leaf = leaf_word(cnt, (leaf & kLeafFirstMask) + 1u);
       } else if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
         leaf = w;
         w = sp ? stk[--sp * kBlock] : kNone;
@@ -802,7 +803,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       FS_WAVE_TRIP(tally.leaf_trips);
       tally.lane_leaves++;
 #endif
-      test_leaf<COUNT, ZLMODE>(S, leaf, oi, r, zl, h, tally);
+      test_leaf<COUNT, ZLMODE>(S, base, leaf, oi, r, zl, h, tally);
       leaf = 0;
       if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
         leaf = w;
@@ -870,7 +871,8 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
     if (o->i3)
       small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
     else
-      traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+      traverse_ww<COUNT>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally, nullptr, false,
+                         0u, 0u, slp);
     const bool wrote = h.obj == (int32_t)oi && before != (int32_t)oi;
     if (TEX && wrote && o->i4) h.tc = (int32_t)oi;  // mesh.cpp:300-311: only with texcoords
     return wrote;
@@ -1082,7 +1084,8 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
         if (visit)
-          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
+          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally,
+                                          ws, resume_here,
                                           o->i5 ? susp_thr : 0u, live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
@@ -1093,7 +1096,8 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
         if (park) continue;
       } else if (visit) {
-        traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+        traverse_ww<COUNT>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally, nullptr, false,
+                           0u, 0u, slp);
       }
       // MeshObject::Trace writes surface_texcoords only when the mesh has
       // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
@@ -1258,7 +1262,7 @@ __device__ __forceinline__ void stale_texcoords(const DevScene& S, const Ray& r,
       m.point = 0;
       m.tc = -1;
       Tally<false> tally;
-      traverse_ww<false>(S, (uint32_t)o->i0, oi, r, zero_len(r), m, stk, tally);
+      traverse_ww<false>(S, (uint32_t)o->i0, __float_as_uint(o->d[6]), oi, r, zero_len(r), m, stk, tally);
       if (m.obj == oi) {
         const float2* q = S.tri_tex + 3 * (size_t)m.prim;
         float2 t0 = q[0], t1 = q[1], t2 = q[2];
@@ -2077,7 +2081,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_PARKED) *why = "unknown schedule";
   else if (o->samples_per_block < 1 || o->samples_per_block > kChunk) *why = "samples_per_block must be 1..64";
   else if (o->xcd_bands > 2) *why = "xcd_bands must be 0, 1 or 2";
-  else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..127";
+  else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..15";
   else if (o->bvh_bins < 2 || o->bvh_bins > 64) *why = "bvh_bins must be 2..64";
   else if (o->node_layout > FS_NODE_LAYOUT_PAIRS) *why = "unknown node_layout";
   else if (o->persist > 1) *why = "persist must be 0 or 1";

@@ -231,7 +231,8 @@ class BvhBuilder {
         mesh_tex_(mesh_tex),
         leaf_(opt.leaf),
         bins_(opt.bins),
-        par_depth_(parallel_depth(opt.threads)) {}
+        par_depth_(parallel_depth(opt.threads)),
+        tri_base_((uint32_t)tris->size()) {}
 
   // Builds the tree over all faces; returns the root node index.
   uint32_t build(std::vector<Prim>& prims, uint32_t* max_depth) {
@@ -290,7 +291,7 @@ class BvhBuilder {
   }
   uint32_t make_leaf(uint32_t b, uint32_t e) {
     if (e - b > kMaxLeafCount) overflow_ = true;  // cannot be encoded: reported by build()
-    uint32_t start = (uint32_t)tris_->size();
+    uint32_t start = (uint32_t)tris_->size() - tri_base_;  // relative to the mesh's first slot
     for (uint32_t i = b; i < e; i++) {
       uint32_t f = (*prims_)[i].face;
       tris_->push_back((*mesh_tris_)[f]);
@@ -300,7 +301,7 @@ class BvhBuilder {
       if (!mesh_tex_->empty())
         tri_tex_->insert(tri_tex_->end(), mesh_tex_->begin() + 6 * (size_t)f, mesh_tex_->begin() + 6 * (size_t)f + 6);
     }
-    return kLeafBit | ((e - b) << 24) | start;
+    return leaf_word(e - b, start);
   }
   // Partitions [b,e) into two halves; returns the split index.
   uint32_t partition(uint32_t b, uint32_t e, uint32_t depth) {
@@ -393,14 +394,14 @@ class BvhBuilder {
   // Appends a local subtree after everything built so far: the result is the
   // same DFS layout the sequential build produces. Returns the subtree root.
   uint32_t merge(Local& L) {
-    const uint32_t node_off = (uint32_t)nodes_->size(), tri_off = (uint32_t)tris_->size();
+    const uint32_t node_off = (uint32_t)nodes_->size(), tri_off = (uint32_t)tris_->size() - tri_base_;
     for (BvhNode n : L.nodes) {
       for (int c = 0; c < 2; c++) {
         uint32_t w = n.child[c];
         if (!(w & kLeafBit))
           n.child[c] = w + node_off;
-        else if ((w >> 24) & 0x7Fu)
-          n.child[c] = (w & ~0xFFFFFFu) | ((w & 0xFFFFFFu) + tri_off);
+        else if (leaf_count(w))
+          n.child[c] = (w & ~kLeafFirstMask) | ((w & kLeafFirstMask) + tri_off);
       }
       nodes_->push_back(n);
     }
@@ -462,6 +463,7 @@ class BvhBuilder {
   uint32_t leaf_;
   int bins_;
   uint32_t par_depth_;
+  uint32_t tri_base_;  // the mesh's first triangle slot: leaf words count from it
   uint32_t max_depth_ = 0;
   bool overflow_ = false;
 };
@@ -873,7 +875,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   }
   // A BVH2 over n faces has at most n-1 inner nodes: size the arrays once
   // (regrowing a 1 M-face scene's arrays costs tens of ms of copies).
-  if (all_tris <= kMaxTriangles) {
+  if (all_tris <= (1ull << 31)) {
     S.nodes.reserve(all_tris + d->num_meshes);
     S.tris.reserve(all_tris);
     if (any_normals) S.tri_normals.reserve(12 * all_tris);
@@ -982,8 +984,13 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     mesh_out[mi].texcoords = nt > 0;
     mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
     if (!mesh_out[mi].tree) continue;
-    if (S.tris.size() + S.deferred_tris + m.num_triangles > kMaxTriangles) {
-      *err = "too many triangles for the 24-bit leaf encoding";
+    if (m.num_triangles > kMaxMeshTriangles) {
+      *err = "mesh " + std::to_string(mi) + ": more than 2^27 triangles (the leaf encoding's limit per mesh)";
+      return FS_ERR_INVALID;
+    }
+    if (S.tris.size() + S.deferred_tris + m.num_triangles >= (1ull << 31) ||
+        S.nodes.size() + S.deferred_nodes + m.num_triangles >= (1ull << 31)) {
+      *err = "scene has 2^31 or more triangles or BVH nodes (31-bit node and triangle indices)";
       return FS_ERR_INVALID;
     }
     for (DevTri& t : mtris) t.mesh_obj = mi;
@@ -1042,7 +1049,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
                    std::chrono::duration<double, std::milli>(tb - tp).count(),
                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
     if (mesh_out[mi].root == 0xFFFFFFFFu) {
-      *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 127 triangles at the depth bound";
+      *err = "mesh " + std::to_string(mi) + ": BVH leaf exceeds 15 triangles at the depth bound";
       return FS_ERR_INVALID;
     }
   }
@@ -1056,6 +1063,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.node_base = nb;
       D.tri_base = tb;
       mesh_out[D.mesh].root = nb;
+      mesh_out[D.mesh].first_tri = tb;
       nb += D.num_tris;
       tb += D.num_tris;
     }
@@ -1086,7 +1094,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
       D.i3 = (int32_t)mo.small;
-      if (mo.small) std::memcpy(&D.d[6], &mo.first_tri, 4);
+      std::memcpy(&D.d[6], &mo.first_tri, 4);  // leaf words and small meshes count from here
       D.i4 = mo.texcoords ? 1 : 0;
       D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);

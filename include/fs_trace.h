@@ -244,7 +244,7 @@ typedef struct fs_options {
   uint32_t xcd_bands;          /* 2 whole 64x64 tiles per XCD (2), 1 one band per XCD, 0 none */
   uint32_t gpu_bvh_min_tris;   /* FS_UPLOAD_GPU_BVH: meshes this large build on the device
                                   (65536; never below 1024) */
-  uint32_t bvh_leaf;           /* faces per BVH leaf, 1..127 (2) */
+  uint32_t bvh_leaf;           /* faces per BVH leaf, 1..15 (2) */
   uint32_t bvh_bins;           /* SAH bins per axis, 2..64 (16) */
   uint32_t bvh_threads;        /* host BVH build threads, 0 = 16 (0) */
   uint32_t node_layout;        /* FS_NODE_LAYOUT_* of host-built trees (DEPTH_FIRST) */

@@ -55,7 +55,7 @@ def test_options_defaults_and_validation_without_device():
     assert lib.fs_options_default(None) == -1
     assert lib.fs_set_options(None, C.byref(o)) == -1
     d, n = C.c_uint64(), C.c_uint64()
-    for bad in ({"bvh_leaf": 0}, {"bvh_bins": 65}, {"samples_per_block": 65}, {"schedule": 3}, {"xcd_bands": 3},
+    for bad in ({"bvh_leaf": 0}, {"bvh_leaf": 16}, {"bvh_bins": 65}, {"samples_per_block": 65}, {"schedule": 3}, {"xcd_bands": 3},
                 {"persist": 2}, {"small_mesh_tris": 65}):
         ob = fsamd.options(**bad)
         assert lib.fs_prepare_digest(C.c_void_p(1), C.byref(ob), C.byref(d), C.byref(n), None) == -1, bad

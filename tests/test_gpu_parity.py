@@ -796,3 +796,55 @@ def test_object_octree_loaded_scene_and_trace_range(tmp_path, gpu_renderer):
     o = oracle_py.Scene(s.desc_ptr())
     np.testing.assert_array_equal(gpu_renderer.trace_range(cam, 80, 60, pts), o.trace_range(cam, 80, 60, pts))
     o.close()
+
+
+# ---- meshes beyond 2^24 triangles ---------------------------------------
+def _giant_blob_scene(filler):
+    """The first object: `filler` copies of one far-away triangle at negative
+    coordinates (the BVH's root split puts them first, so the blob's faces
+    land in triangle slots >= filler) followed by a visible blob; then the
+    Cornell room. filler = 0 gives the blob alone."""
+    import scenes
+
+    b = DescBuilder()
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(15, 15, 15))
+    clay = b.material(fsamd.MAT_CERAMIC, diffuse=(0.75, 0.6, 0.45), shininess=0.6)
+    bv, bf = scenes.blob_mesh(nu=64, nv=32, radius=4.0)
+    bv = bv + np.array([0.0, 8.0, 2.0])
+    if filler:
+        far = np.array([[-1e6, -1e6, -1e6], [-1e6 + 1, -1e6, -1e6], [-1e6, -1e6 + 1, -1e6]])
+        verts = np.concatenate([far, bv])
+        faces = np.concatenate([np.tile(np.array([[0, 1, 2]], np.int32), (filler, 1)), bf + 3])
+    else:
+        verts, faces = bv, bf
+    b.mesh(clay, verts, faces)
+    cornell_room(b, white, red, light)
+    return b
+
+
+def test_mesh_beyond_2_24_triangles(gpu_renderer):
+    """Leaf words count from the mesh's first triangle slot with 27 bits
+    (fs_scene.h), so one mesh may hold more than 2^24 triangles, as the
+    reference's meshes may (mesh.cpp:242-272). Mesh A = 2^24 filler faces
+    plus a blob whose faces sit at slots >= 2^24 (device BVH build, parked
+    walks); B = the blob alone. Both are the first object, so every segment
+    that meets the blob walks them: the frames are identical on every plane,
+    and B's frame is the oracle's bit for bit."""
+    W, H, spp = 64, 48, 4
+    small = _giant_blob_scene(0)
+    ptr = small.build()
+    ref_gpu = gpu_render(gpu_renderer, ptr, CAM, W, H, spp)
+    assert_parity(ref_gpu, oracle_render(ptr, CAM, W, H, spp), exact=True)
+    giant = _giant_blob_scene(1 << 24)
+    gpu_renderer.upload(giant.build(), gpu_bvh=True)
+    stats = gpu_renderer.scene_stats()
+    assert stats["triangles"] > (1 << 24) + 4096
+    f = gpu_renderer.frame(W, H)
+    gpu_renderer.render(CAM, f, spp=spp)
+    assert "true" in gpu_renderer.last_kernel().split(",")[3]  # the parked-walk kernel
+    for p in range(6):
+        np.testing.assert_array_equal(f.read(p), ref_gpu[p], err_msg=f"plane {p}")
+    f.close()
+    del giant
