@@ -582,7 +582,7 @@ __global__ void k_emit(Build B, uint32_t ntasks, uint32_t small_max) {
     const uint32_t f = fate_of(B, T, cnt);
     if (f == 0u) {
       if (cnt > kMaxLeafCount) atomicOr(&B.counters[4], 1u);
-      word = leaf_word(cnt, cb);  // relative to the mesh's first slot (B.tri_base)
+      word = leaf_word(cnt, B.tri_base + cb);
     } else if (f == 1u) {
       const uint32_t base = node, i = small++;  // a binary tree over cnt: <= cnt-1 inner nodes
       node += cnt - 1;
@@ -800,7 +800,7 @@ __global__ __launch_bounds__(64) void k_small(Build B, uint32_t nsmall) {
       uint32_t word;
       if (cnt <= B.leaf || depth + 1 >= kGuard) {
         if (cnt > kMaxLeafCount) flags |= 1u;
-        word = leaf_word(cnt, root.b + rb[s]);
+        word = leaf_word(cnt, B.tri_base + root.b + rb[s]);
       } else {
         const uint32_t c = next++;
         if (sp >= (int)kTraversalStack + 2 || c >= root.node + (n0 - 1)) {

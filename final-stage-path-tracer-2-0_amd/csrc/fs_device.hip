@@ -643,10 +643,10 @@ __device__ __forceinline__ void tri_candidate(const DevScene& S, const TriData& 
 }
 
 template <bool COUNT, int ZLMODE = -1>  // ZLMODE: 0/1 = ray known (non-)zero-length, -1 = runtime zl
-__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t base, uint32_t w, int32_t oi, const Ray& r,
-                                          bool zl_rt, MinHit& h, Tally<COUNT>& tally) {
+__device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t oi, const Ray& r, bool zl_rt, MinHit& h,
+                                          Tally<COUNT>& tally) {
   const bool zl = ZLMODE < 0 ? zl_rt : ZLMODE == 1;
-  uint32_t cnt = leaf_count(w), first = base + (w & kLeafFirstMask);  // global triangle slot
+  uint32_t cnt = leaf_count(w), first = w & kLeafFirstMask;
   for (uint32_t i = 0; i < cnt; i++) {
     uint32_t ti = first + i;
     TriData T = load_tri(S.tris, ti);
@@ -701,8 +701,7 @@ __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) {
 // moves on and they resume from *ws in a later iteration (same operations in
 // the same order per lane).
 template <bool COUNT, bool SUSP = false, int ZLMODE = -1>  // ZLMODE as in test_leaf
-__device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, uint32_t base, int32_t oi, const Ray& r,
-                                            bool zl_rt,
+__device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, int32_t oi, const Ray& r, bool zl_rt,
                                             MinHit& h, uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                             WalkSuspend* ws = nullptr, bool resume = false, uint32_t thr = 0,
                                             uint32_t live = 0, const Slopes* pre = nullptr) {
@@ -785,7 +784,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, ui
 #endif
       uint32_t cnt = leaf_count(leaf);
       if (cnt) {
-        test_leaf<COUNT, ZLMODE>(S, base, leaf_word(1, leaf & kLeafFirstMask), oi, r, zl, h, tally);
+        test_leaf<COUNT, ZLMODE>(S, leaf_word(1, leaf & kLeafFirstMask), oi, r, zl, h, tally);
         cnt--;
       }
       if (cnt) {
@@ -803,7 +802,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, ui
       FS_WAVE_TRIP(tally.leaf_trips);
       tally.lane_leaves++;
 #endif
-      test_leaf<COUNT, ZLMODE>(S, base, leaf, oi, r, zl, h, tally);
+      test_leaf<COUNT, ZLMODE>(S, leaf, oi, r, zl, h, tally);
       leaf = 0;
       if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
         leaf = w;
@@ -871,8 +870,7 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
     if (o->i3)
       small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
     else
-      traverse_ww<COUNT>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally, nullptr, false,
-                         0u, 0u, slp);
+      traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
     const bool wrote = h.obj == (int32_t)oi && before != (int32_t)oi;
     if (TEX && wrote && o->i4) h.tc = (int32_t)oi;  // mesh.cpp:300-311: only with texcoords
     return wrote;
@@ -1084,8 +1082,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
         if (visit)
-          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally,
-                                          ws, resume_here,
+          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
                                           o->i5 ? susp_thr : 0u, live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
@@ -1096,8 +1093,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
         if (park) continue;
       } else if (visit) {
-        traverse_ww<COUNT>(S, (uint32_t)o->i0, __float_as_uint(d[6]), (int32_t)oi, r, zl, h, stk, tally, nullptr, false,
-                           0u, 0u, slp);
+        traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
       }
       // MeshObject::Trace writes surface_texcoords only when the mesh has
       // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
@@ -1262,7 +1258,7 @@ __device__ __forceinline__ void stale_texcoords(const DevScene& S, const Ray& r,
       m.point = 0;
       m.tc = -1;
       Tally<false> tally;
-      traverse_ww<false>(S, (uint32_t)o->i0, __float_as_uint(o->d[6]), oi, r, zero_len(r), m, stk, tally);
+      traverse_ww<false>(S, (uint32_t)o->i0, oi, r, zero_len(r), m, stk, tally);
       if (m.obj == oi) {
         const float2* q = S.tri_tex + 3 * (size_t)m.prim;
         float2 t0 = q[0], t1 = q[1], t2 = q[2];
@@ -1386,6 +1382,18 @@ __device__ __forceinline__ TaskBlock decode_block(const Launch& P, const DevFram
   return B;
 }
 
+// A kernel-argument record read through a pointer offset by `zero`, a
+// wave-uniform 0 the compiler cannot prove to be 0 (derived from the block
+// cursor), so its loads stay at their uses. Read directly, the records the
+// persistent loop needs only now and then (the camera basis, the block
+// decode, the sky and AOV fields) were hoisted out of the loop and held in
+// SGPRs for the whole kernel: about 100 SGPRs spilled into VGPR lanes, and
+// reads of spilled scene pointers landed in the BVH node loop.
+template <class T>
+__device__ __forceinline__ const T& at_use(const T& v, uint32_t zero) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(&v) + zero);
+}
+
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kQueueStride = 64;  // work-queue counters 256 B apart
 
@@ -1493,9 +1501,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       uint32_t served = 0;
       while (served < nfree) {
         if (cur.next >= cur.total) {
-          const uint32_t b = fetch_block(P, queues, queue, queues_left);
+          const uint32_t z = cur.sample0 >> 31;  // 0 (sample indices stay below 2^20)
+          const uint32_t b = fetch_block(at_use(P, z), queues, queue, queues_left);
           if (b == kNoBlock) break;
-          cur = decode_block(P, F, b);
+          cur = decode_block(at_use(P, z), at_use(F, z), b);
         } else {
           const uint32_t take = min(nfree - served, cur.total - cur.next);
           if (fresh && rank - served < take) {
@@ -1504,7 +1513,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
             const uint32_t k = task - s * cur.nvalid, px = k % cur.vx, py = k / cur.vx;
             x = cur.x0 + px;
             y = cur.y0 + py;
-            pix = y * F.width + x;
+            pix = y * at_use(F, cur.sample0 >> 31).width + x;
             smp = cur.sample0 + s;
             rad_row = cur.rad_row;
             slot = (s * kBlock + py * 8 + px) | ((cur.aov && s == P.spp - 1) ? 0x80000000u : 0u);
@@ -1518,7 +1527,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     }
     if (fresh) {
       rng = pixel_seed(pix, smp, P.seed);
-      r = camera_ray(C, (float)x, (float)y, rng);
+      r = camera_ray(at_use(C, cur.sample0 >> 31), (float)x, (float)y, rng);
       depth = 0;
       mats.reset();
       top = -1;
@@ -1579,19 +1588,21 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         // the walk is parked; the lane resumes it next iteration
       } else if (h.obj < 0) {
         if (depth == 1) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
-        L = mk3(S.sky_r, S.sky_g, S.sky_b);
-        if (TEX && S.sky_tex) {  // textured Light sky: SampleSky (scene.cpp:157-162, engine.cpp:91-92)
+        const DevScene& Sz = at_use(S, cur.sample0 >> 31);
+        L = mk3(Sz.sky_r, Sz.sky_g, Sz.sky_b);
+        if (TEX && Sz.sky_tex) {  // textured Light sky: SampleSky (scene.cpp:157-162, engine.cpp:91-92)
           float tu, tv;
           sphere_tc(normalize(r.stop - r.start), tu, tv);
-          L = sample_tex(S, S.materials[S.sky], tu, tv) * 3.0f;
+          L = sample_tex(S, S.materials[Sz.sky], tu, tv) * 3.0f;
         }
         if (depth == 0 && aov) {  // the last sample's AOVs remain
+          const DevFrame& Fz = at_use(F, cur.sample0 >> 31);
           f3 nd = normalize(r.dir);
-          at_byte(F.normal, pix * 12u)[0] = nd.x;
-          at_byte(F.normal, pix * 12u)[1] = nd.y;
-          at_byte(F.normal, pix * 12u)[2] = nd.z;
-          *at_byte(F.depth, pix * 4u) = C.z_far;
-          *at_byte(F.material, pix * 8u) = S.sky_id;
+          at_byte(Fz.normal, pix * 12u)[0] = nd.x;
+          at_byte(Fz.normal, pix * 12u)[1] = nd.y;
+          at_byte(Fz.normal, pix * 12u)[2] = nd.z;
+          *at_byte(Fz.depth, pix * 4u) = C.z_far;
+          *at_byte(Fz.material, pix * 8u) = Sz.sky_id;
         }
         done = true;
       } else {
@@ -1619,11 +1630,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         top = (int)depth;
         if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
         if (depth == 0 && aov) {
-          at_byte(F.normal, pix * 12u)[0] = nn.x;
-          at_byte(F.normal, pix * 12u)[1] = nn.y;
-          at_byte(F.normal, pix * 12u)[2] = nn.z;
-          *at_byte(F.depth, pix * 4u) = length(r.start - p);
-          *at_byte(F.material, pix * 8u) = m.id;
+          const DevFrame& Fz = at_use(F, cur.sample0 >> 31);
+          at_byte(Fz.normal, pix * 12u)[0] = nn.x;
+          at_byte(Fz.normal, pix * 12u)[1] = nn.y;
+          at_byte(Fz.normal, pix * 12u)[2] = nn.z;
+          *at_byte(Fz.depth, pix * 4u) = length(r.start - p);
+          *at_byte(Fz.material, pix * 8u) = m.id;
         }
         bool use = mat_will_use(m, refl, nn);
         Ray nr;

@@ -231,8 +231,7 @@ class BvhBuilder {
         mesh_tex_(mesh_tex),
         leaf_(opt.leaf),
         bins_(opt.bins),
-        par_depth_(parallel_depth(opt.threads)),
-        tri_base_((uint32_t)tris->size()) {}
+        par_depth_(parallel_depth(opt.threads)) {}
 
   // Builds the tree over all faces; returns the root node index.
   uint32_t build(std::vector<Prim>& prims, uint32_t* max_depth) {
@@ -291,7 +290,7 @@ class BvhBuilder {
   }
   uint32_t make_leaf(uint32_t b, uint32_t e) {
     if (e - b > kMaxLeafCount) overflow_ = true;  // cannot be encoded: reported by build()
-    uint32_t start = (uint32_t)tris_->size() - tri_base_;  // relative to the mesh's first slot
+    uint32_t start = (uint32_t)tris_->size();
     for (uint32_t i = b; i < e; i++) {
       uint32_t f = (*prims_)[i].face;
       tris_->push_back((*mesh_tris_)[f]);
@@ -394,7 +393,7 @@ class BvhBuilder {
   // Appends a local subtree after everything built so far: the result is the
   // same DFS layout the sequential build produces. Returns the subtree root.
   uint32_t merge(Local& L) {
-    const uint32_t node_off = (uint32_t)nodes_->size(), tri_off = (uint32_t)tris_->size() - tri_base_;
+    const uint32_t node_off = (uint32_t)nodes_->size(), tri_off = (uint32_t)tris_->size();
     for (BvhNode n : L.nodes) {
       for (int c = 0; c < 2; c++) {
         uint32_t w = n.child[c];
@@ -463,7 +462,6 @@ class BvhBuilder {
   uint32_t leaf_;
   int bins_;
   uint32_t par_depth_;
-  uint32_t tri_base_;  // the mesh's first triangle slot: leaf words count from it
   uint32_t max_depth_ = 0;
   bool overflow_ = false;
 };
@@ -875,7 +873,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   }
   // A BVH2 over n faces has at most n-1 inner nodes: size the arrays once
   // (regrowing a 1 M-face scene's arrays costs tens of ms of copies).
-  if (all_tris <= (1ull << 31)) {
+  if (all_tris <= kMaxTriangles) {
     S.nodes.reserve(all_tris + d->num_meshes);
     S.tris.reserve(all_tris);
     if (any_normals) S.tri_normals.reserve(12 * all_tris);
@@ -984,13 +982,8 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     mesh_out[mi].texcoords = nt > 0;
     mesh_out[mi].tree = need && !verts.empty() && m.num_triangles > 0;  // mesh.cpp:119-121
     if (!mesh_out[mi].tree) continue;
-    if (m.num_triangles > kMaxMeshTriangles) {
-      *err = "mesh " + std::to_string(mi) + ": more than 2^27 triangles (the leaf encoding's limit per mesh)";
-      return FS_ERR_INVALID;
-    }
-    if (S.tris.size() + S.deferred_tris + m.num_triangles >= (1ull << 31) ||
-        S.nodes.size() + S.deferred_nodes + m.num_triangles >= (1ull << 31)) {
-      *err = "scene has 2^31 or more triangles or BVH nodes (31-bit node and triangle indices)";
+    if (S.tris.size() + S.deferred_tris + m.num_triangles > kMaxTriangles) {
+      *err = "scene has more than 2^27 triangles (the leaf encoding's 27-bit first-triangle slot)";
       return FS_ERR_INVALID;
     }
     for (DevTri& t : mtris) t.mesh_obj = mi;

@@ -39,15 +39,16 @@ struct DevObject {
   // QUAD    d0-3 plane, d4-6 origin, d7 half width, d8 half height,
   //         d9-11 bitangent, d12-14 tangent
   // MESH    d0-5 reference root bounds (min, max) — mesh.cpp:129-133;
-  //         d6 (uint bits) the mesh's first triangle slot (leaf words are relative to it)
+  //         d6 (uint bits) the mesh's first triangle slot (small meshes: their faces)
 };
 static_assert(sizeof(DevObject) == 192, "DevObject layout");
 
 // BVH2 node, 64 B: both child boxes (SoA over the two children) + child words.
 // Child word: bit31 set -> leaf, bits 27..30 = triangle count (<= 15), bits
-// 0..26 = first triangle relative to the mesh's first triangle slot
-// (DevObject::d[6]); otherwise an inner-node index (31 bits). A mesh holds at
-// most 2^27 triangles; a scene any number of meshes.
+// 0..26 = first triangle slot; otherwise an inner-node index (31 bits). A
+// scene holds at most 2^27 triangles. (First slots relative to each mesh, with
+// the mesh's base added per walk, cost C4 5.6 %: the extra live value spilled
+// the scene pointers' SGPRs into VGPR lanes read in the node loop.)
 struct BvhNode {
   float lo_x[2], hi_x[2];
   float lo_y[2], hi_y[2];
@@ -60,12 +61,15 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kLeafCountShift = 27;
 constexpr uint32_t kLeafFirstMask = (1u << kLeafCountShift) - 1;
 constexpr uint32_t kMaxLeafCount = 15;
-constexpr uint32_t kMaxMeshTriangles = 1u << kLeafCountShift;
+constexpr uint32_t kMaxTriangles = 1u << kLeafCountShift;  // per scene
 FS_HD uint32_t leaf_word(uint32_t count, uint32_t first) {
   return kLeafBit | (count << kLeafCountShift) | first;
 }
 FS_HD uint32_t leaf_count(uint32_t w) { return (w >> kLeafCountShift) & 0xFu; }
-constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces)
+#ifndef FS_STACK
+#define FS_STACK 24  // (other values are A/B builds: the LDS stack bounds the waves per CU)
+#endif
+constexpr uint32_t kTraversalStack = FS_STACK;  // BVH depth bound (builder enforces)
 constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
 // Triangle record: the operands of the reference test (intersect.cpp:357-419)
