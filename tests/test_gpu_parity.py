@@ -825,9 +825,9 @@ def _giant_blob_scene(filler):
 
 
 def test_mesh_beyond_2_24_triangles(gpu_renderer):
-    """Leaf words count from the mesh's first triangle slot with 27 bits
-    (fs_scene.h), so one mesh may hold more than 2^24 triangles, as the
-    reference's meshes may (mesh.cpp:242-272). Mesh A = 2^24 filler faces
+    """Leaf words hold a 27-bit first-triangle slot (fs_scene.h), so a scene
+    (and one mesh) may hold more than 2^24 triangles, as the reference's
+    meshes may (mesh.cpp:242-272). Mesh A = 2^24 filler faces
     plus a blob whose faces sit at slots >= 2^24 (device BVH build, parked
     walks); B = the blob alone. Both are the first object, so every segment
     that meets the blob walks them: the frames are identical on every plane,
