@@ -1526,7 +1526,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       if (fresh && !got) break;  // every queue is empty: this lane is done
     }
     if (fresh) {
-      rng = pixel_seed(pix, smp, P.seed);
+      rng = pixel_seed(pix, smp, at_use(P, cur.sample0 >> 31).seed);
       r = camera_ray(at_use(C, cur.sample0 >> 31), (float)x, (float)y, rng);
       depth = 0;
       mats.reset();
