@@ -234,6 +234,7 @@ struct TriData {
   float d00, d01, d11, inv;
   uint32_t axis, face;
   f4 pl;
+  bool same_plane;  // small meshes: the previous slot's face has the same plane bits
 };
 __device__ __forceinline__ TriData unpack_tri(float4 a, float4 b, float4 c, float4 d) {
   TriData t;
@@ -247,6 +248,7 @@ __device__ __forceinline__ TriData unpack_tri(float4 a, float4 b, float4 c, floa
   const uint32_t fa = __float_as_uint(c.z);
   t.face = fa & 0x3FFFFFFFu;
   t.axis = fa >> 30;
+  t.same_plane = (__float_as_uint(c.w) & kSamePlaneBit) != 0;
   t.d00 = d.x;
   t.d01 = d.y;
   t.d11 = d.z;
@@ -291,6 +293,7 @@ struct TriData {
   float d00, d01, d11, inv;
   uint32_t axis, face;
   f4 pl;
+  bool same_plane;
 };
 __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
   const float4* q = reinterpret_cast<const float4*>(T + i);
@@ -306,6 +309,7 @@ __device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32
   t.inv = d.y;
   t.axis = __float_as_uint(d.z);
   t.pl = mk4(e.x, e.y, e.z, e.w);
+  t.same_plane = (__float_as_uint(d.w) & kSamePlaneBit) != 0;
   return t;
 }
 __device__ __forceinline__ TriData load_tri_uniform(const DevTri* T, uint32_t i) { return load_tri(T, i); }
@@ -660,14 +664,43 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
 // and the closest hit is a total order on (t, face), so testing all faces
 // gives the walk's hit bit for bit; the faces come in SGPRs, not as
 // dependent per-lane node and triangle fetches.
+// A face whose plane has the previous face's bits (the two triangles of a
+// quad) reuses its plane test: intersect.cpp:728-744 on identical operands.
 template <bool COUNT>
 __device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
                                                  const Ray& r, bool zl, MinHit& h, Tally<COUNT>& tally) {
+  bool on_plane = false;  // the plane test of the last distinct plane
+  float tt = 0.0f;
+  f3 pp = mk3(0, 0, 0);
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t ti = first + i;
     TriData T = load_tri_uniform(S.tris, ti);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.utris++;
-    tri_candidate(S, T, ti, oi, r, zl, h);
+    if (!T.same_plane || i == 0) {  // wave-uniform
+      if (!zl) {
+        on_plane = ray_plane(T.pl, r, tt, pp);
+      } else {  // point_in_tri's plane part (intersect.cpp:320-346)
+        const float d4 = T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w * 1.0f;
+        on_plane = cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon);
+        tt = 0.0f;
+        pp = r.start;
+      }
+    }
+    if (on_plane) {
+      float uu, vv;
+      bary_pre(T, FS_BARY_ARG(pp, T), uu, vv);
+      if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
+        bool better = tt < h.t || (tt == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
+        if (better) {
+          h.t = tt;
+          h.obj = oi;
+          h.prim = ti;
+          h.u = uu;
+          h.v = vv;
+          h.point = zl ? 1u : 0u;
+        }
+      }
+    }
   }
 }
 

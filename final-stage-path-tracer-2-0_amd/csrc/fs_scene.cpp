@@ -1036,6 +1036,12 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
     auto tb = std::chrono::steady_clock::now();
     mesh_out[mi].root = builder.build(prims, &S.max_depth);
     if (pairs && mesh_out[mi].root == node_begin) relayout_pairs(&S.nodes, node_begin);
+    if (mesh_out[mi].small) {  // faces whose plane has the previous slot's bits share its plane test
+      const uint32_t f0 = mesh_out[mi].first_tri;
+      for (uint32_t f = f0 + 1; f < f0 + m.num_triangles; f++)
+        if (!std::memcmp(S.tris[f].plane, S.tris[f - 1].plane, sizeof(S.tris[f].plane)))
+          S.tris[f].mesh_obj |= kSamePlaneBit;
+    }
     if (opt.log)
       std::fprintf(stderr, "[fs build] mesh %u: %u tris, prepare %.1f ms, prims %.1f ms, bvh %.1f ms\n", mi,
                    m.num_triangles, std::chrono::duration<double, std::milli>(tp - t0).count(),
@@ -1087,7 +1093,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i1 = mo.normals ? 1 : 0;
       D.i2 = mo.tree ? 1 : 0;
       D.i3 = (int32_t)mo.small;
-      std::memcpy(&D.d[6], &mo.first_tri, 4);  // leaf words and small meshes count from here
+      std::memcpy(&D.d[6], &mo.first_tri, 4);  // small meshes: their faces from here
       D.i4 = mo.texcoords ? 1 : 0;
       D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
       put3(D.d, mo.rb.mn);

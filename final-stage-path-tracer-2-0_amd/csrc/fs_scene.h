@@ -91,10 +91,11 @@ struct DevTri {
   float v0[2];
   float v1[2];
   uint32_t face_axis;
-  uint32_t mesh_obj;
+  uint32_t mesh_obj;  // mesh index; bit 31 (small meshes): the same plane bits as the previous slot's face
   float d00, d01, d11, inv;
 };
 static_assert(sizeof(DevTri) == 64, "DevTri layout");
+constexpr uint32_t kSamePlaneBit = 0x80000000u;
 inline uint32_t tri_face_host(const DevTri& t) { return t.face_axis & 0x3FFFFFFFu; }
 #else
 // 80 B: full 3-vectors (A/B builds with -DFS_TRI64=0).
