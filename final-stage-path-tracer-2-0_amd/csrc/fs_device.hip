@@ -415,30 +415,50 @@ __device__ __forceinline__ float pow50(float xf) {
   return (float)(x32 * x16 * x2);
 }
 
-// Material::Reflection (material.cpp)
+// Material::Reflection (material.cpp). The kinds that scatter around a
+// table normal (Diffuse, Metal, Glass's reflection, Ceramic, Glow) differ
+// only in the solid angle: the per-kind switch picks it, with each kind's
+// own RNG draws in their order, and the lanes of a mixed wave then run ONE
+// random_reflection together instead of one copy per kind.
 __device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, f3 view, f3 n, uint64_t& rng) {
+  enum { kScatter, kZero, kMirror, kRefract, kFrosted, kView };
+  int mode = kScatter;
+  float solid = kPi;
   switch (m.kind) {
     case FS_MAT_LIGHT:
-      return mk3(0, 0, 0);
+      mode = kZero;
+      break;
     case FS_MAT_DIFFUSE:
-      return random_reflection(S, view, n, kPi, rng);
+      break;
     case FS_MAT_METAL:
-      return random_reflection(S, view, n, kPi * m.roughness, rng);
+      solid = kPi * m.roughness;
+      break;
     case FS_MAT_MIRROR:
-      return reflect(view, n);
+      mode = kMirror;
+      break;
     case FS_MAT_GLASS:
-      if (rng_float(rng) < m.reflectivity) return random_reflection(S, view, n, kPi * m.frost, rng);
-      return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
+      if (rng_float(rng) < m.reflectivity)
+        solid = kPi * m.frost;
+      else
+        mode = kFrosted;
+      break;
     case FS_MAT_LIQUID:
-      if (rng_float(rng) < m.reflectivity) return reflect(view, n);
-      return refract(view, n, m.index);
+      mode = rng_float(rng) < m.reflectivity ? kMirror : kRefract;
+      break;
     case FS_MAT_CERAMIC:
     case FS_MAT_GLOW:
-      if (rng_float(rng) < 0.1f) return random_reflection(S, view, n, 0.0f, rng);
-      return random_reflection(S, view, n, (float)((double)kPi * (1.0 - (double)m.shininess)), rng);
+      solid = rng_float(rng) < 0.1f ? 0.0f : (float)((double)kPi * (1.0 - (double)m.shininess));
+      break;
     default:  // FS_MAT_FOG
-      return view;
+      mode = kView;
+      break;
   }
+  if (mode == kScatter) return random_reflection(S, view, n, solid, rng);
+  if (mode == kMirror) return reflect(view, n);
+  if (mode == kRefract) return refract(view, n, m.index);
+  if (mode == kFrosted) return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
+  if (mode == kView) return view;
+  return mk3(0, 0, 0);
 }
 __device__ __forceinline__ bool mat_will_use(const fs_material& m, f3 r, f3 n) {
   switch (m.kind) {
@@ -1428,6 +1448,7 @@ __device__ __forceinline__ const T& at_use(const T& v, uint32_t zero) {
 }
 
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+constexpr uint32_t kFog0 = 0x40000000u;  // slot bit: the first hit is Fog
 constexpr uint32_t kQueueStride = 64;  // work-queue counters 256 B apart
 
 // The wave's next block. One-shot waves (P.persist 0) take block
@@ -1495,7 +1516,9 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   // the lane's task: its pixel, sample and radiance slot
   uint32_t x = 0, y = 0, pix = 0, smp = 0;
   uint32_t rad_row = 0;
-  uint32_t slot = 0;  // s * kBlock + 8 * py + px, bit 31: this sample leaves the AOVs
+  // s * kBlock + 8 * py + px; bit 31: this sample leaves the AOVs; bit 30
+  // (kFog0): the path's first hit is Fog, so its two anchors are kept
+  uint32_t slot = 0;
   uint64_t rng = 0;
   Ray r;
   uint32_t depth = 0;
@@ -1564,8 +1587,6 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       depth = 0;
       mats.reset();
       top = -1;
-      *at_byte(anchor, a0_off) = make_float4(0, 0, 0, 0);
-      *at_byte(anchor, a1_off) = make_float4(0, 0, 0, 0);
       fresh = false;
     }
     FS_PHASE(1);
@@ -1620,7 +1641,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       if (SUSP && parked) {
         // the walk is parked; the lane resumes it next iteration
       } else if (h.obj < 0) {
-        if (depth == 1) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
+        if (depth == 1 && (slot & kFog0)) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
         const DevScene& Sz = at_use(S, cur.sample0 >> 31);
         L = mk3(Sz.sky_r, Sz.sky_g, Sz.sky_b);
         if (TEX && Sz.sky_tex) {  // textured Light sky: SampleSky (scene.cpp:157-162, engine.cpp:91-92)
@@ -1643,7 +1664,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         int32_t mi;
         float tu, tv;
         rebuild_hit<TEX>(S, r, h, p, nn, mi, tu, tv, stk);
-        if (depth == 1) *at_byte(anchor, a1_off) = make_float4(p.x, p.y, p.z, 0);
+        if (depth == 1 && (slot & kFog0)) *at_byte(anchor, a1_off) = make_float4(p.x, p.y, p.z, 0);
         const fs_material& m = S.materials[mi];
         if (TEX && m.texture >= 0) {
           f3 tx = sample_tex(S, m, tu, tv);
@@ -1661,7 +1682,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         *at_byte(lvl, (depth * kBlock + lane) * 8u) = make_float2(c, ds);
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
-        if (depth == 0) *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
+        if (depth == 0 && kind == FS_MAT_FOG) {  // Fog draws with the distance of its two anchors
+          *at_byte(anchor, a0_off) = make_float4(p.x, p.y, p.z, 0);
+          slot |= kFog0;
+        }
         if (depth == 0 && aov) {
           const DevFrame& Fz = at_use(F, cur.sample0 >> 31);
           at_byte(Fz.normal, pix * 12u)[0] = nn.x;
@@ -1688,14 +1712,14 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     FS_PHASE(3);
     if (done) {
       f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-      if (top >= 0 && S.materials[mats.get(0)].kind == FS_MAT_FOG) {
+      if (slot & kFog0) {  // both anchors were written (a Fog hit always bounces on to depth 1)
         float4 a = *at_byte(anchor, a0_off), b = *at_byte(anchor, a1_off);
         p0 = mk3(a.x, a.y, a.z);
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX, MMAT>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
       float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);  // [channel][sample][pixel]
-      const uint32_t o = slot & 0x7FFFFFFFu;
+      const uint32_t o = slot & ~(0x80000000u | kFog0);
       rad[o] = L.x;
       rad[P.spp * kBlock + o] = L.y;
       rad[2 * P.spp * kBlock + o] = L.z;
