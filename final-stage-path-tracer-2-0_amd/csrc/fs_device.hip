@@ -548,29 +548,46 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
 
 // texrow: per-level SampleDiffuse result of a textured material (lean kernel
 // only; other schedules pass nullptr and never see a textured scene).
+// The loads of level k-1 (its material's kind and colour, its c) are issued
+// before level k is applied, so the serial chain of the backward pass waits
+// on one cache round trip per path instead of one per level.
 template <bool TEX = false, bool MMAT = false>
 __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const MatTrail<MMAT>& mats,
                                      const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
                                      int stride = kBlock, uint32_t lane = 0,
                                      const float4* __restrict__ texrow = nullptr) {
+  if (top < 0) return L;
+  const float* cv = reinterpret_cast<const float*>(lvl);
+  // c = max(0, n.r) of every kind: [level][lane]; Ceramic's specular term: [kMaxDepth + level][lane]
+  const fs_material* mp = &S.materials[mats.get(top)];
+  int32_t kind = mp->kind;
+  f3 dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
+  float c = *at_byte(cv, ((uint32_t)top * (uint32_t)stride + lane) * 4u);
   for (int k = top; k >= 0; --k) {
-    const fs_material& m = S.materials[mats.get(k)];
-    float2 cs = *at_byte(lvl, ((uint32_t)k * (uint32_t)stride + lane) * 8u);
-    f3 dif = mk3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
-    f3 sd = dif;  // SampleDiffuse (material.cpp:108-126)
+    const fs_material& m = *mp;
+    const int32_t kk = kind;
+    const f3 dk = dif;
+    const float ck = c;
+    if (k > 0) {  // next level's loads, in flight while this level is applied
+      mp = &S.materials[mats.get(k - 1)];
+      kind = mp->kind;
+      dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
+      c = *at_byte(cv, ((uint32_t)(k - 1) * (uint32_t)stride + lane) * 4u);
+    }
+    f3 sd = dk;  // SampleDiffuse (material.cpp:108-126)
     if (TEX && m.texture >= 0) {
       float4 tx = *at_byte(texrow, ((uint32_t)k * (uint32_t)stride + lane) * 16u);
       sd = mk3(tx.x, tx.y, tx.z);
     }
-    switch (m.kind) {
+    switch (kk) {
       case FS_MAT_LIGHT:  // material.cpp:43-53
         L = (TEX && m.texture >= 0) ? sd : mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
         break;
       case FS_MAT_DIFFUSE:
-        L = (sd * L) * cs.x;
+        L = (sd * L) * ck;
         break;
       case FS_MAT_METAL: {
-        f3 dc = (sd * L) * cs.x;
+        f3 dc = (sd * L) * ck;
         f3 rc = sd * L;
         L = dc * m.roughness + rc * (float)(1.0 - (double)m.roughness);
         break;
@@ -578,13 +595,14 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
       case FS_MAT_MIRROR:
       case FS_MAT_GLASS:
       case FS_MAT_LIQUID:
-        L = L * dif;
+        L = L * dk;
         break;
       case FS_MAT_CERAMIC:
       case FS_MAT_GLOW: {
-        f3 dc = (sd * L) * cs.x;
-        L = L * cs.y + dc * (float)(1.0 - (double)cs.y);
-        if (m.kind == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
+        const float ds = *at_byte(cv, ((kMaxDepth + (uint32_t)k) * (uint32_t)stride + lane) * 4u);
+        f3 dc = (sd * L) * ck;
+        L = L * ds + dc * (float)(1.0 - (double)ds);
+        if (kk == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
         break;
       }
       default:  // FS_MAT_FOG (material.cpp:319-339)
@@ -593,15 +611,13 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
           float x = (dist * dist) * m.density * 0.00005f;
           float mx = (0.0f < x) ? x : 0.0f;
           float th = (mx < 0.0f) ? 0.0f : (mx > 1.0f ? 1.0f : mx);
-          if (rng_float(rng) < th) L = dif;
+          if (rng_float(rng) < th) L = dk;
         }
         break;
     }
   }
-  if (top >= 0) {  // engine.cpp:147-151
-    const fs_material& m0 = S.materials[mats.get(0)];
-    if (length(L) > 10.0f && m0.kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
-  }
+  // engine.cpp:147-151 (kind holds level 0's: the loop ends on it)
+  if (length(L) > 10.0f && kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
   return L;
 }
 
@@ -1679,7 +1695,9 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
-        *at_byte(lvl, (depth * kBlock + lane) * 8u) = make_float2(c, ds);
+        *at_byte(reinterpret_cast<float*>(lvl), (depth * kBlock + lane) * 4u) = c;  // [level][lane]
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)  // [kMaxDepth + level][lane]
+          *at_byte(reinterpret_cast<float*>(lvl), ((kMaxDepth + depth) * kBlock + lane) * 4u) = ds;
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0 && kind == FS_MAT_FOG) {  // Fog draws with the distance of its two anchors
