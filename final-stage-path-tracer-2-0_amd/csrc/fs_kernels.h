@@ -17,7 +17,7 @@ namespace fs {
 
 constexpr int kBlock = 64;  // one wave64 per block: stacks are per-lane LDS columns
 #ifndef FS_CHUNK
-#define FS_CHUNK 64  // C4 +1.5 % over 32 (shorter task-pool tails per block), 16 -2 %
+#define FS_CHUNK 64  // the largest samples_per_block (default 16: the task pool runs on across blocks)
 #endif
 constexpr uint32_t kChunk = FS_CHUNK;  // samples per pixel per block (fs_render splits longer renders)
 // Scenes with at most this many materials pack a path's per-bounce material
