@@ -139,7 +139,12 @@ def zoo(frost=0.0):
     return b
 
 
-def test_material_and_object_zoo_bit_exact(gpu_renderer):
+@pytest.mark.parametrize("schedule", ["auto", "parked"])
+def test_material_and_object_zoo_bit_exact(schedule, gpu_renderer):
+    """Every material and object kind. The lean kernel applies Material::Sample
+    as straight-line selects, the parked-walk kernel as a per-kind switch:
+    both are held to the oracle."""
+    gpu_renderer.set_options(schedule=schedule, park_min_tris=1)
     b = zoo(frost=0.0)
     ptr = b.build()
     out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
