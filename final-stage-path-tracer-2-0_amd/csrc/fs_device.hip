@@ -1614,8 +1614,17 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           const uint32_t take = min(nfree - served, cur.total - cur.next);
           if (fresh && rank - served < take) {
             const uint32_t task = cur.next + (rank - served);
-            const uint32_t s = task / cur.nvalid;
-            const uint32_t k = task - s * cur.nvalid, px = k % cur.vx, py = k / cur.vx;
+            uint32_t s, px, py;
+            if (cur.nvalid == 64) {  // a whole 8x8 micro-tile (wave-uniform): shifts, not divisions
+              s = task >> 6;
+              px = task & 7u;
+              py = (task >> 3) & 7u;
+            } else {  // a micro-tile cut by the frame edge
+              s = task / cur.nvalid;
+              const uint32_t k = task - s * cur.nvalid;
+              px = k % cur.vx;
+              py = k / cur.vx;
+            }
             x = cur.x0 + px;
             y = cur.y0 + py;
             pix = y * at_use(F, cur.sample0 >> 31).width + x;
