@@ -1143,6 +1143,7 @@ template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
+                                                uint32_t susp_thr_small = 0,
                                                 bool* parked = nullptr) {
   if (SOCT) {  // Scene::Trace with a valid object tree (scene.cpp:231-236)
     scene_trace_tree<COUNT, TEX>(S, r, h, stk, tally);
@@ -1187,7 +1188,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         // branch out of the loop, measured 3-4 % slower: code size)
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
-                                          o->i5 ? susp_thr : 0u, live, slp);
+                                          o->i5 == 2 ? susp_thr : (o->i5 ? susp_thr_small : 0u), live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
         if (park) {
@@ -1664,7 +1665,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
       const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
-      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small, &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
@@ -1695,7 +1696,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       tk = __builtin_readcyclecounter();  // the histogram's own time is left out
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, &parked);
+      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small, &parked);
 #endif
       FS_PHASE(2);
       if (SUSP && parked) {
@@ -2282,7 +2283,8 @@ int fs_options_default(fs_options* o) {
   if (!o) return fail(FS_ERR_INVALID, "null options");
   *o = fs_options{};
   o->schedule = FS_SCHEDULE_AUTO;
-  o->park_lanes = 10;  // C4: 8-10 best at 6 waves per SIMD
+  o->park_lanes = 10;       // C4 (1 M-face blob): 10-12 best
+  o->park_lanes_small = 6;  // C3 (38 k and 209 k-face meshes): 4-6 best
   o->park_min_tris = kParkMinTris;
   o->samples_per_block = 16;  // persistent waves: C4 +0.7 %, C3 +2 %, C2 +3 % over 64 (8 and 4 no better)
   o->groups = 0;
@@ -2521,6 +2523,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.seed = params->seed;
   const fs_options& O = ctx->opt;
   L.susp_thr = O.park_lanes;
+  L.susp_thr_small = O.park_lanes_small;
   // XCD placement: 0 dispatch order, 1 one band per XCD (C4 -25 %: the bands
   // are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
   L.xcd_bands = O.xcd_bands;

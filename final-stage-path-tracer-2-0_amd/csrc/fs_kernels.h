@@ -80,7 +80,9 @@ struct DevCounters {
 struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;
   uint32_t sample_base, spp;
-  uint32_t susp_thr;  // SUSP schedule: park walks when at most this many lanes still walk
+  uint32_t susp_thr;        // SUSP schedule: park walks of a mesh of >= kParkLargeTris faces when at most
+                            // this many lanes still walk
+  uint32_t susp_thr_small;  // the same for the smaller parkable meshes
   uint32_t xcd_bands;  // 1: each XCD (blocks b, b+8, ...) renders one contiguous band of micro-tiles
   // Sample groups: one launch renders `groups` consecutive runs of `spp`
   // samples; block (g, micro-tile) takes samples sample_base + g*spp ...

@@ -1095,7 +1095,8 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       D.i3 = (int32_t)mo.small;
       std::memcpy(&D.d[6], &mo.first_tri, 4);  // small meshes: their faces from here
       D.i4 = mo.texcoords ? 1 : 0;
-      D.i5 = d->meshes[o.mesh].num_triangles >= park_min ? 1 : 0;
+      const uint32_t nt = d->meshes[o.mesh].num_triangles;
+      D.i5 = nt >= park_min ? (nt >= kParkLargeTris ? 2 : 1) : 0;
       put3(D.d, mo.rb.mn);
       put3(D.d + 3, mo.rb.mx);
       obj_bounds[i] = mo.rb;

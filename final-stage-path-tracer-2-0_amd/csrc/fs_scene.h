@@ -18,7 +18,8 @@ namespace fs {
 // schedule (fs_device.hip): measured on MI355X, parking pays for the ~1M
 // triangle C4 blob (+15%) and loses on the ~250k-triangle C3 atrium (-4%,
 // meshes of 60-120k triangles), so only scenes with such a mesh select it.
-constexpr uint32_t kParkMinTris = 1u << 19;
+constexpr uint32_t kParkMinTris = 1u << 15;    // meshes whose walks may park (fs_options default)
+constexpr uint32_t kParkLargeTris = 1u << 19;  // parkable meshes from here use park_lanes, below park_lanes_small
 
 struct DevObject {
   int32_t kind;  // fs_object_kind (QUAD_PUV is stored as QUAD_ONWH)
@@ -29,7 +30,7 @@ struct DevObject {
   int32_t i3;    // MESH: n > 0 for a small mesh of n triangles (fs_options.small_mesh_tris),
                  // tested face by face from triangle d[6] (bits) on, without a walk
   int32_t i4;    // MESH: 1 if the mesh has texcoords (mesh.cpp:300)
-  int32_t i5;    // MESH: 1 if its walks may park (>= kParkMinTris triangles, SUSP schedule)
+  int32_t i5;    // MESH: walks may park (SUSP schedule): 0 never, 1 under kParkLargeTris triangles, 2 from there
   float d[40];
   // SPHERE  d0-2 center, d3 radius
   // PLANE   d0-3 plane

@@ -97,7 +97,7 @@ class fs_options(C.Structure):
                 ("tile_order", C.c_uint32), ("xcd_bands", C.c_uint32), ("gpu_bvh_min_tris", C.c_uint32),
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
-                ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32)]
+                ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 3
+#define FS_ABI_VERSION 4
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -235,8 +235,9 @@ typedef enum fs_schedule {
 
 typedef struct fs_options {
   int32_t schedule;            /* fs_schedule (AUTO) */
-  uint32_t park_lanes;         /* PARKED: park when at most this many lanes still walk (10) */
-  uint32_t park_min_tris;      /* meshes whose walks may park (2^19); read at upload */
+  uint32_t park_lanes;         /* PARKED: park when at most this many lanes still walk a mesh of
+                                  >= 2^19 triangles (10) */
+  uint32_t park_min_tris;      /* meshes whose walks may park (32768); read at upload */
   uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (16) */
   uint32_t groups;             /* sample groups per launch; 0 = sized to >= 262144 blocks (0) */
   uint32_t group_major;        /* block order: 0 a tile's groups together (0), 1 group by group */
@@ -254,6 +255,7 @@ typedef struct fs_options {
   uint32_t small_mesh_tris;    /* host-built meshes of at most this many triangles are tested
                                   face by face with wave-uniform loads, no BVH walk (16; 0 off,
                                   max 64); read at upload */
+  uint32_t park_lanes_small;   /* PARKED: park_lanes for parkable meshes under 2^19 triangles (6) */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */

@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_abi_version_and_errors_without_device():
     lib = fsamd.gpu_lib()
-    assert lib.fs_abi_version() == 3
+    assert lib.fs_abi_version() == 4
     assert lib.fs_upload_scene(None, None) == -1  # FS_ERR_INVALID
     assert b"null" in lib.fs_last_error()
     assert lib.fs_render(None, None, None, None) == -1
@@ -45,10 +45,10 @@ def test_options_defaults_and_validation_without_device():
     (checked by fs_prepare_digest, which needs no device)."""
     o = fsamd.options()
     d = fsamd.options_dict(o)
-    assert d == {"schedule": 0, "park_lanes": 10, "park_min_tris": 1 << 19, "samples_per_block": 16, "groups": 0,
+    assert d == {"schedule": 0, "park_lanes": 10, "park_min_tris": 1 << 15, "samples_per_block": 16, "groups": 0,
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
-                 "small_mesh_tris": 16}
+                 "small_mesh_tris": 16, "park_lanes_small": 6}
     assert fsamd.parse_variant("schedule=parked@park_lanes=8") == {"schedule": "parked", "park_lanes": 8}
     assert fsamd.options(schedule="parked").schedule == 2
     lib = fsamd.gpu_lib()

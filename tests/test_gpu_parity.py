@@ -79,10 +79,10 @@ def test_scene_parity(name, dims, scene_dir, gpu_renderer):
     W, H, spp = dims
     s = load_scene(name, scene_dir)
     out = gpu_render(gpu_renderer, s, s.camera(0), W, H, spp)
-    # only C4 has a mesh large enough (>= 2^19 triangles) for parked walks
+    # C3 and C4 hold meshes large enough (>= park_min_tris, 2^15 faces) for parked walks
     k = gpu_renderer.last_kernel()
     parked = k.startswith("render_kernel_lean<false, ") and k[:-1].split(", ")[3] == "true"  # <.., waves, TEX, SUSP, MMAT>
-    assert parked == (name == "c4"), gpu_renderer.last_kernel()
+    assert parked == (name in ("c3", "c4")), gpu_renderer.last_kernel()
     ref = oracle_render(s.desc_ptr(), s.camera(0), W, H, spp)
     assert_parity(out, ref, exact=True)
 
@@ -561,7 +561,8 @@ OPTION_VARIANTS = [
     {},
     {"schedule": "lean"},
     {"schedule": "parked", "park_min_tris": 1},
-    {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63},
+    {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63, "park_lanes_small": 63},
+    {"schedule": "parked", "park_min_tris": 1, "park_lanes_small": 1},
     {"samples_per_block": 64},
     {"samples_per_block": 7},
     {"xcd_bands": 0},
