@@ -22,18 +22,25 @@
 #include "fs_scene.h"
 #include "fs_trace.h"
 
-// Wave priority inside BVH walks (s_setprio): waves in a walk issue first,
-// so the dependent node fetches of the latency-bound walks start sooner
-// (C2 +1.3 %, C3 +0.8 %, C4 neutral; 1 and 3 measure the same; 0 = off)
 #ifndef FS_FLAT_LEAF  // leaf tests one triangle per trip over both leaves (A/B)
 #define FS_FLAT_LEAF 1
 #endif
+// Wave priority inside BVH walks (s_setprio): waves in a walk issue first,
+// so the dependent node fetches of the latency-bound walks start sooner
+// (C2 +1.3 %, C3 +0.8 %, C4 neutral; 1 and 3 measure the same; 0 = off)
 #ifndef FS_TRAV_PRIO
 #define FS_TRAV_PRIO 1
 #endif
 // BVH-walk slab constants once per segment (1) or once per mesh walk (0, A/B)
 #ifndef FS_HOIST_SLOPES
 #define FS_HOIST_SLOPES 1
+#endif
+// Slab exit clamp to the walk's t limit as a signed-integer min on the float
+// bits (1) instead of fminf (0, A/B): the limit is positive, so the integer
+// order is the float order for every finite exit, and v_min_f32 needed the
+// loop-carried limit re-canonicalised on every node trip.
+#ifndef FS_SLAB_IMIN
+#define FS_SLAB_IMIN 1
 #endif
 
 namespace fs {
@@ -842,9 +849,16 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
         float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
         float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
+#if FS_SLAB_IMIN
+        const int tl = __float_as_int(tmax_lim);
+        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), __int_as_float(min(__float_as_int(fmaxf(g0, k0)), tl)));
+        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
+        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), __int_as_float(min(__float_as_int(fmaxf(g1, k1)), tl)));
+#else
         float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
         float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
         float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
+#endif
         h0 = n0 <= f0;
         h1 = n1 <= f1;
         t0 = n0;
@@ -870,7 +884,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       // and the check ran with a nearly idle wave).
       if (SUSP) {
         const uint32_t walkers = (uint32_t)__popcll(__builtin_amdgcn_read_exec());
-        if (walkers <= thr && walkers < live) {
+        if (walkers <= thr && walkers < (uint32_t)__builtin_amdgcn_readfirstlane(live)) {
           susp = true;
           break;
         }
