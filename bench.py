@@ -47,7 +47,8 @@ WORKLOADS = {
 }
 # Algorithmic bytes per unit of work, from the device SoA record
 # sizes: BVH node 64 B and triangle 64 B (fs_scene.h DevTri), both per lane;
-# an object record 128 B per WAVE (the object loop reads records with scalar
+# an object test 128 B per WAVE (the fields a test reads, at most a cuboid's
+# planes + box + kind/material, of the 192-B record; the object loop reads them with scalar
 # loads at a wave-uniform index: one load serves the 64 lanes), and so are
 # the 64-B triangle records of small meshes (fs_options.small_mesh_tris); per segment
 # one material record (76 B) + one normal-table entry (16 B); per sample 12 B
