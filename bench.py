@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -39,6 +40,7 @@ fsamd.host_lib()
 
 METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080, 1024spp; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_LANE_OPS_PEAK = 1024 * 32 * 2.4e9  # 157.3 TF FP32 vector peak / 2 (an FMA is one lane-op)
 WORKLOADS = {
     "c4": "~1M-triangle displaced blob + Ceramic/Glass spheres + Metal cuboid in the Cornell room "
           "(BASELINE configs[3] scene; SURVEY §8d C4) at 1920x1080, 1024 spp",
@@ -54,6 +56,10 @@ WORKLOADS = {
 # one material record (76 B) + one normal-table entry (16 B); per sample 12 B
 # of radiance.
 S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
+# tools/cpu_calibration.py, survey container, 8 threads, against the reference rates
+# of SURVEY.md §6 [probe]
+CPU_CALIBRATION = ("restatement/reference rate 1.03 on C4 1080p (8 threads, survey container; DESIGN §6): "
+                   "the baseline stands for the reference on C4")
 
 
 def parse():
@@ -89,7 +95,17 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     group = rendezvous.FileGroup(rank, world) if world > 1 else None
+    try:
+        run(args, rank, world, local_rank, group)
+    except BaseException:
+        if group:
+            group.abort()  # no stale files for a later launch; rank 0 removes the directory
+        raise
+    if group:
+        group.close()
 
+
+def run(args, rank, world, local_rank, group):
     scene_dir = args.scene_dir or os.path.join(tempfile.gettempdir(), f"fs_bench_{os.getuid()}_r{rank}")
     t0 = time.time()
     path = scenes.write(args.scene, os.path.join(scene_dir, args.scene))
@@ -109,20 +125,31 @@ def main():
     W, H, spp = args.width, args.height, args.spp
     frame = r.frame(W, H)
     params = fsamd.render_params(W, H, spp, tile_offset=rank, tile_stride=world)
+    rccl_ranks = None
     if group:
         uid = group.broadcast(fsamd.Renderer.comm_unique_id() if rank == 0 else None, root=0)
         r.comm_init(world, rank, uid)
+        rccl_ranks = r.comm_count()
 
     def step():
+        """One step: render (HIP-event time of the trace launches), then for
+        N > 1 the RCCL gather, timed on the host from the end of this rank's
+        render to the end of the gather (it includes waiting for slower ranks)."""
         frame.reset()
         r.render(cam, frame, spp=spp, tile_offset=rank, tile_stride=world, sync=False)
+        g_ms = 0.0
         if world > 1:
+            r.synchronize()
+            tg = time.perf_counter()
             r.gather(frame, params, root=0)
-        r.synchronize()
-        return r.last_render_ms()
+            r.synchronize()
+            g_ms = (time.perf_counter() - tg) * 1e3
+        else:
+            r.synchronize()
+        return r.last_render_ms(), g_ms
 
     for i in range(args.warmup):
-        ms = step()
+        ms, _ = step()
         log(f"rank {rank}: warmup {i} render {ms:.1f} ms")
 
     def barrier():
@@ -131,77 +158,133 @@ def main():
 
     barrier()
     r.synchronize()
-    kernel_ms = []
+    kernel_ms, gather_ms = [], []
     t_start = time.perf_counter()
     for i in range(args.steps):
-        kernel_ms.append(step())
-        log(f"rank {rank}: step {i} render {kernel_ms[-1]:.1f} ms")
+        k_ms, g_ms = step()
+        kernel_ms.append(k_ms)
+        gather_ms.append(g_ms)
+        log(f"rank {rank}: step {i} render {k_ms:.1f} ms gather {g_ms:.1f} ms")
     r.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed_local = time.perf_counter() - t_start
     kernel_name = r.last_kernel()
     launches, launch_spp = r.last_launches()
+    per_rank = None
+    elapsed = elapsed_local
     if group:
-        elapsed = group.max(elapsed)
+        rows = group.allgather([elapsed_local, sum(kernel_ms) / len(kernel_ms), sum(gather_ms) / len(gather_ms)])
+        per_rank = per_rank_stats(rows, rccl_ranks)
+        elapsed = max(row[0] for row in rows)
 
     # ---- roofline of the trace kernel: algorithmic bytes from a counted launch
-    total_samples = W * H * spp * args.steps
-    value = total_samples / elapsed / 1e6
     cf = r.frame(W, H)
     cspp = 8
     r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
     c = r.counters()
     cf.close()
-    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * (c["tri_tests"] + c["small_tri_loads"])
-                        + S_OBJ * c["object_loads"] + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
-    avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
-    owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
-    per_launch_bytes = bytes_per_sample * owned_samples / launches
-    achieved = per_launch_bytes / avg_launch_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{W}x{H}.json")
-    if os.path.exists(pmc):  # PMC passes of tools/gpu_pmc.sh, per sample of the same kernel
-        try:
-            pm = json.load(open(pmc))
-            if kernel_name in pm.get("kernel", "") and pm.get("hbm_bytes_per_sample"):
-                traffic = round(pm["hbm_bytes_per_sample"] * owned_samples / launches)
-        except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                # the same launch time against the PMC-measured bytes (FETCH x2 + WRITE per launch)
-                "traffic_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic else None,
-                "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-                "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                "launches_per_step": launches, "spp_per_launch": launch_spp,
-                "bytes_per_sample": round(bytes_per_sample, 1),
-                "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
-                "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),
-                "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2),
-                "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
-                "small_tri_loads_per_sample": round(c["small_tri_loads"] / max(c["samples"], 1), 3),
-                "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
+    roofline = make_roofline(args.scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, scene, cam)
 
     if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded procedural scene, per-(pixel,sample) seeded xorshift64*)",
-            "config": {"workload": WORKLOADS[args.scene], "scene": args.scene, "width": W, "height": H,
-                       "spp": spp, "triangles": stats["triangles"], "bvh_nodes": stats["nodes"],
-                       "bvh_build_ms": round(stats["build_ms"], 1), "bvh_builder": args.bvh,
-                       "parallelism": f"64x64 tiles round-robin over {world} GPU(s)"
-                                      + (" + RCCL ncclGather to rank 0" if world > 1 else "")},
-            "roofline": roofline, "cpu_baseline": cpu,
-        }
+        out = make_record(args, world, elapsed, stats, roofline, cpu, per_rank)
         print(json.dumps(out), flush=True)
-    if group:
-        group.close()
+
+
+def per_rank_stats(rows, rccl_ranks):
+    """The N > 1 self-check fields from every rank's [timed-region s, mean
+    render ms, mean gather ms] (rendezvous allgather, rank order): whether a
+    loss of scaling is render imbalance or the gather."""
+    render = [round(row[1], 2) for row in rows]
+    return {"rccl_ranks": rccl_ranks, "render_ms": render, "gather_ms": [round(row[2], 2) for row in rows],
+            "timed_s": [round(row[0], 4) for row in rows],
+            "slowest_rank": max(range(len(rows)), key=lambda i: rows[i][1]),
+            "render_imbalance": round(max(render) / max(min(render), 1e-9), 4)}
+
+
+def pmc_record(scene, W, H, kernel_name):
+    """The committed PMC summary of this kernel on this workload (tools/gpu_pmc.sh +
+    tools/pmc_summary.py), or None: the run replays it, it does not measure it."""
+    path = os.path.join("profiles", f"pmc_{scene}_{W}x{H}.json")
+    try:
+        pm = json.load(open(os.path.join(ROOT, path)))
+    except (OSError, ValueError):
+        return None, path
+    if kernel_name not in pm.get("kernel", ""):
+        return None, path
+    return pm, path
+
+
+def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp):
+    bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * (c["tri_tests"] + c["small_tri_loads"])
+                        + S_OBJ * (c["object_loads"] + c.get("lane_object_loads", 0))
+                        + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
+    avg_launch_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3 / launches
+    owned_samples = c["samples"] / cspp * spp  # samples this rank renders per step
+    per_launch_bytes = bytes_per_sample * owned_samples / launches
+    achieved = per_launch_bytes / avg_launch_s / 1e9
+    hbm_frac = achieved / HBM_PEAK_GBS
+    pm, pm_path = pmc_record(scene, W, H, kernel_name)
+    traffic = None
+    valu = None
+    if pm and pm.get("hbm_bytes_per_sample"):
+        traffic = round(pm["hbm_bytes_per_sample"] * owned_samples / launches)
+    if pm and pm.get("valu_insts_per_sample"):
+        # VALU against the gfx950 peak, replayed per sample from the PMC file onto this
+        # run's launch time: issue = wave64 VALU instructions x 2 cycles (32-lane SIMD,
+        # MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc) over the 1024 SIMDs' cycles at
+        # the clock the PMC run measured (GRBM_GUI_ACTIVE / 8 / launch time); lane-op rate =
+        # active lanes x instructions against 1024 SIMDs x 32 lanes x 2.4 GHz (= 157.3 TF / 2)
+        insts = pm["valu_insts_per_sample"] * owned_samples / launches
+        clock = pm.get("clock_ghz") or 2.4
+        issue_frac = insts * 2 / (1024 * clock * 1e9 * avg_launch_s)
+        lane_ops = insts * 64 * pm["valu_lane_util"]
+        lane_frac = lane_ops / avg_launch_s / VALU_LANE_OPS_PEAK
+        valu = {"valu_busy": round(issue_frac, 4), "valu_lane_util": pm["valu_lane_util"],
+                "valu_lane_op_frac": round(lane_frac, 4), "clock_ghz": clock,
+                "wait_any_frac": pm.get("wait_any_frac")}
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(hbm_frac, 4), "traffic": traffic,
+            "traffic_source": pm_path + " (replayed per sample, not measured by this run)" if traffic else None,
+            # the same launch time against the PMC-measured bytes (FETCH x2 + WRITE per launch)
+            "traffic_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic else None,
+            "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "valu": valu,
+            "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+            "launches_per_step": launches, "spp_per_launch": launch_spp,
+            "bytes_per_sample": round(bytes_per_sample, 1),
+            "segments_per_sample": round(c["segments"] / max(c["samples"], 1), 3),
+            "nodes_per_segment": round(c["node_visits"] / max(c["segments"], 1), 2),
+            "tris_per_segment": round(c["tri_tests"] / max(c["segments"], 1), 2),
+            "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
+            "small_tri_loads_per_sample": round(c["small_tri_loads"] / max(c["samples"], 1), 3),
+            "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
+    if valu and valu["valu_busy"] > hbm_frac:
+        roof["bound"] = "valu"  # the larger of the two fractions names the binding resource
+    return roof
+
+
+def make_record(args, world, elapsed, stats, roofline, cpu, per_rank=None):
+    W, H, spp = args.width, args.height, args.spp
+    value = W * H * spp * args.steps / elapsed / 1e6
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded procedural scene, per-(pixel,sample) seeded xorshift64*)",
+        "config": {"workload": WORKLOADS[args.scene], "scene": args.scene, "width": W, "height": H,
+                   "spp": spp, "triangles": stats["triangles"], "bvh_nodes": stats["nodes"],
+                   "bvh_build_ms": round(stats["build_ms"], 1), "bvh_builder": args.bvh,
+                   "parallelism": f"64x64 tiles round-robin over {world} GPU(s)"
+                                  + (" + RCCL ncclGather to rank 0" if world > 1 else "")},
+        "roofline": roofline, "cpu_baseline": cpu,
+    }
+    if per_rank is not None:
+        out["ranks"] = per_rank
+    return out
 
 
 def host_cpus():
@@ -222,9 +305,21 @@ def host_cpus():
     return {"nproc": nproc, "affinity": aff, "quota": quota}
 
 
+def effective_cpus(hw):
+    """CPUs the baseline may really use: the affinity set, capped by the cgroup
+    quota (a 16-CPU quota on a 256-thread host is 16 CPUs of work)."""
+    n = hw["affinity"]
+    if hw["quota"]:
+        n = min(n, max(1, math.ceil(hw["quota"])))
+    return n
+
+
 def cpu_baseline(args, scene, cam):
     """The oracle (CPU port of the reference algorithm, reference octree)
-    timed on a bounded tile subset of the same workload."""
+    timed on a bounded tile subset of the same workload: with one thread per
+    CPU the process may use (`value`, `cores`), and, reference-style, with one
+    thread per hardware thread of the affinity set (engine.cpp:174,261-274:
+    hardware_concurrency() bands; `value_all_threads`)."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
@@ -235,11 +330,16 @@ def cpu_baseline(args, scene, cam):
         stride = args.cpu_tile_stride
         p = fsamd.render_params(args.width, args.height, args.cpu_spp, tile_stride=stride, tile_offset=0)
         hw = host_cpus()
-        threads = args.cpu_threads if args.cpu_threads > 0 else hw["affinity"]
-        t = time.perf_counter()
-        f = o.render(cam, p, threads=threads)
-        dt = time.perf_counter() - t
-        n = f.stats["samples"]
+        cores = args.cpu_threads if args.cpu_threads > 0 else effective_cpus(hw)
+
+        def timed(threads):
+            t0 = time.perf_counter()
+            f = o.render(cam, p, threads=threads)
+            return f.stats["samples"], time.perf_counter() - t0
+
+        n, dt = timed(cores)
+        all_threads = hw["affinity"]
+        n_all, dt_all = (n, dt) if all_threads == cores else timed(all_threads)
         o.close()
         cpu_model = ""
         try:
@@ -249,13 +349,14 @@ def cpu_baseline(args, scene, cam):
                     break
         except OSError:
             pass
-        return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+        return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+                "value_all_threads": round(n_all / dt_all / 1e6, 4), "threads_all": all_threads,
                 "nproc": hw["nproc"], "affinity_cpus": hw["affinity"], "cgroup_cpu_quota": hw["quota"],
                 "sample": f"{args.scene} {args.width}x{args.height}, 1/{stride} of the 64x64 tiles, "
-                          f"{args.cpu_spp} spp = {n} samples in {dt:.1f}s (octree build {build:.1f}s excluded)",
+                          f"{args.cpu_spp} spp = {n} samples in {dt:.1f}s on {cores} threads "
+                          f"(octree build {build:.1f}s excluded)",
                 "cpu": cpu_model or platform.processor(),
-                "calibration": "restatement/reference rate 1.03 on C4 1080p (8 threads, survey container; "
-                               "DESIGN §6): the baseline stands for the reference on C4 only"}
+                "calibration": CPU_CALIBRATION}
     except Exception as e:  # the baseline is reported, never required
         log(f"cpu baseline failed: {e}")
         return None

@@ -42,6 +42,24 @@
 #ifndef FS_SLAB_IMIN
 #define FS_SLAB_IMIN 1
 #endif
+// Mesh-root cull: the rcp slab decision is redone with the reference's
+// divisions only when a cross-slab pair of entry/exit params is close (1), or
+// whenever the entry and exit params are close (0, A/B: every hit on a flat
+// box, e.g. a Cornell wall, took the exact path).
+#ifndef FS_ROOT_PAIRS
+#define FS_ROOT_PAIRS 1
+#endif
+// Radiance rows of a block: [sample][pixel][rgb], one 12-B store per sample
+// (1), or [rgb][sample][pixel], three 4-B stores 1 KiB apart (0, A/B). The
+// rows are written once, by lanes that finish in different iterations, so
+// their lines leave L2 partly written: measured write traffic 50 B per 12-B
+// sample with the planar layout.
+#ifndef FS_RAD_XYZ
+#define FS_RAD_XYZ 1
+#endif
+#ifndef FS_RAD_NT
+#define FS_RAD_NT 0
+#endif
 
 namespace fs {
 namespace dev {
@@ -181,8 +199,42 @@ __device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool 
   f3 s = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
   f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
   f3 v = e - s;
-  float fnear = -kInfinity, ffar = kInfinity;
   bool outside = false;
+#if FS_ROOT_PAIRS
+  // Per-slab entry/exit (a slab parallel to the segment: +-1e30, never close
+  // to anything). The reference's test fnear > ffar is max(n_i) > min(f_j);
+  // for i == j, n_i <= f_i holds exactly in both (the same product sorted, or
+  // one product twice for a flat box), so only the cross-slab pairs can flip:
+  // the decision is unsure only when one of them is close. A flat box (a wall,
+  // a quad light: n_i = f_i) no longer counts as unsure wherever it is hit.
+  float n[3], f[3];
+  auto slab = [&](int i, float sa, float va, float lo, float hi) {
+    if (cmp_eps(va, 0.0f, kEpsilon)) {
+      outside |= (sa < lo || sa > hi);
+      n[i] = -1e30f;
+      f[i] = 1e30f;
+      return;
+    }
+    float rc = __builtin_amdgcn_rcpf(va);
+    float t1 = (lo - sa) * rc, t2 = (hi - sa) * rc;
+    n[i] = fminf(t1, t2);
+    f[i] = fmaxf(t1, t2);
+  };
+  slab(0, s.x, v.x, mn.x, mx.x);
+  slab(1, s.y, v.y, mn.y, mx.y);
+  slab(2, s.z, v.z, mn.z, mx.z);
+  const float fnear = fmaxf(fmaxf(n[0], n[1]), fmaxf(n[2], -kInfinity));
+  const float ffar = fminf(fminf(f[0], f[1]), f[2]);
+  if (outside || ffar < 0 || fnear < 0) return false;  // exact tests
+  auto close = [](float a, float b) { return fabsf(a - b) <= 1e-5f * (fabsf(a) + fabsf(b)); };
+  // fnear and ffar far apart: certain (as before); close: certain unless a
+  // cross-slab pair is close too (a flat box hit away from its edges)
+  bool unsure = close(fnear, ffar);
+  if (unsure)
+    unsure = close(n[0], f[1]) || close(n[0], f[2]) || close(n[1], f[0]) || close(n[1], f[2]) ||
+             close(n[2], f[0]) || close(n[2], f[1]);
+#else
+  float fnear = -kInfinity, ffar = kInfinity;
   auto slab = [&](float sa, float va, float lo, float hi) {
     if (cmp_eps(va, 0.0f, kEpsilon)) {
       outside |= (sa < lo || sa > hi);
@@ -198,6 +250,7 @@ __device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool 
   slab(s.z, v.z, mn.z, mx.z);
   if (outside || ffar < 0 || fnear < 0) return false;  // exact tests
   bool unsure = fabsf(fnear - ffar) <= 1e-5f * (fabsf(fnear) + fabsf(ffar));
+#endif
   if (!unsure && fnear > ffar) return false;
   if (fabsf(fnear - 1.0f) <= 1e-5f)
     unsure = true;
@@ -370,6 +423,7 @@ struct Tally {
   uint32_t nodes = 0, tris = 0, prims = 0;
   uint32_t objs = 0;  // object records read (wave-uniform loads: counted once per wave)
   uint32_t utris = 0;  // small-mesh triangle records read (wave-uniform loads: once per wave)
+  uint32_t lane_objs = 0;  // object records read at a per-lane index (object octree): once per lane
 #ifdef FS_PHASE_PROF
   // wave-level loop trips, counted by the first active lane of each trip
   uint32_t node_trips = 0, leaf_trips = 0, lane_nodes = 0, lane_leaves = 0;
@@ -963,7 +1017,7 @@ __device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, FloatPtr 
 
 #ifdef FS_PHASE_PROF
 struct PhaseAcc {
-  uint64_t cull = 0, trav = 0, prim = 0;
+  uint64_t cull = 0, trav = 0, prim = 0, small = 0;
 };
 #define FS_TICK() __builtin_readcyclecounter()
 #else
@@ -981,7 +1035,9 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
   const DevObject* __restrict__ o = S.objects + oi;
   const float* d = o->d;
   const int32_t kind = o->kind;
-  if (COUNT) tally.objs++;  // per-lane object index: a vector load per lane
+  // per-lane object index (vector loads), counted per lane in its own field:
+  // bench.py's byte model weighs object_loads per wave
+  if (COUNT) tally.lane_objs++;
   if (kind == FS_OBJ_MESH) {
     if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) return false;
     const int32_t before = h.obj;
@@ -1153,7 +1209,7 @@ __device__ void scene_trace_tree(const DevScene& S, const Ray& r, MinHit& h, uin
 // SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
 // resume it in a later call with the same ray: objects before the parked one
 // are skipped on resume (already processed), the rest follow in order.
-template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false>
+template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false, bool NOWALK = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
@@ -1197,12 +1253,33 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       if (o->i3) {  // a small mesh: its faces, no walk (never parks)
         if (visit)
           small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
+#ifdef FS_PHASE_PROF
+        pa.small += FS_TICK() - t1;
+        t1 = FS_TICK();
+#endif
+      } else if (NOWALK) {
+        // every mesh of the scene is small (chosen at upload): no BVH walk
       } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
+        // thresholds: bits 0-7 park a walk when at most this many lanes still
+        // walk; bits 8-15 defer the walk's start (park at the root) while
+        // fewer lanes than this want to walk and other lanes can go on
+        const uint32_t thr = o->i5 == 2 ? susp_thr : (o->i5 ? susp_thr_small : 0u);
+        if (thr >> 8) {
+          const uint32_t want = (uint32_t)__popcll(__ballot(visit));
+          if (visit && !resume_here && want < (thr >> 8) && want < (uint32_t)__builtin_amdgcn_readfirstlane(live)) {
+            ws->oi = (int32_t)oi;  // parked at the root: the walk starts from there on resume
+            ws->w = (uint32_t)o->i0;
+            ws->leaf = 0;
+            ws->sp = 0;
+            park = true;
+            continue;
+          }
+        }
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
-                                          o->i5 == 2 ? susp_thr : (o->i5 ? susp_thr_small : 0u), live, slp);
+                                          thr & 0xFFu, live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
         if (park) {
@@ -1513,6 +1590,20 @@ __device__ __forceinline__ const T& at_use(const T& v, uint32_t zero) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(&v) + zero);
 }
 
+// One sample's radiance, 12 contiguous bytes of its block's radiance row
+// (FS_RAD_NT: a streaming store; the rows are read back only by fold_groups).
+__device__ __forceinline__ void store_rgb(float* p, f3 L) {
+#if FS_RAD_NT
+  __builtin_nontemporal_store(L.x, p);
+  __builtin_nontemporal_store(L.y, p + 1);
+  __builtin_nontemporal_store(L.z, p + 2);
+#else
+  p[0] = L.x;
+  p[1] = L.y;
+  p[2] = L.z;
+#endif
+}
+
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kFog0 = 0x40000000u;  // slot bit: the first hit is Fog
 constexpr uint32_t kQueueStride = 64;  // work-queue counters 256 B apart
@@ -1555,7 +1646,8 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 // pull blocks until every queue is empty: the launch tail is one task
 // path, not one block. Each sample's radiance goes to its block's radiance
 // row; fold_groups folds the rows into the frame in sample order.
-template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false>
+template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false,
+          bool NOWALK = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
@@ -1564,12 +1656,17 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
                                                                      uint32_t* __restrict__ mat_all,
                                                                      uint32_t* __restrict__ queues,
                                                                      DevCounters* __restrict__ counters) {
-  __shared__ uint32_t stk_all[kTraversalStack * kBlock];
+  // NOWALK (every mesh small): no walk stack; the per-bounce shading scalars
+  // (c and Ceramic's term, [level][lane]) are staged in LDS instead of HBM
+  // scratch rows, so the backward pass reads them at LDS latency and the L2
+  // no longer holds (and writes back) the rows.
+  __shared__ uint32_t stk_all[NOWALK ? 1 : kTraversalStack * kBlock];
+  __shared__ float2 lvl_lds[NOWALK ? kMaxDepth * kBlock : 1];
   const uint32_t lane = threadIdx.x;
   uint32_t* stk = stk_all + lane;
   // Scratch rows of the wave, depth-major ([level][lane]) so a wave's store
   // is one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
-  float2* lvl = lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
+  float2* lvl = NOWALK ? lvl_lds : lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
   float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
   float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
@@ -1596,7 +1693,9 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   MinHit h;         // persists across iterations while a walk is parked (SUSP)
   WalkSuspend ws;
 #ifdef FS_PHASE_PROF
-  uint64_t ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // lane activity per iteration (wave-uniform sums): lanes tracing, shading, unwinding; unwind level trips
+  uint64_t act[4] = {0, 0, 0, 0};
   uint64_t tk = __builtin_readcyclecounter(), t_begin = tk;
 #define FS_PHASE(i)                                 \
   do {                                              \
@@ -1678,12 +1777,17 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       bool parked = false;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
+#ifdef FS_PHASE_HIST
       const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
-      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small, &parked);
+#endif
+      scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
+                                                        &parked);
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
+      ph[10] += pa.small;
       FS_PHASE(2);
+#ifdef FS_PHASE_HIST
       {  // histogram of node visits per traced segment: 0,1-4,5-8,9-16,17-32,33-64,65-128,>128
         uint32_t nv = tally.lane_nodes - nodes_before, bin = 0;
         if (nv > 0) bin = 1;
@@ -1707,10 +1811,16 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           atomicAdd(&counters->phase[25], (unsigned long long)red[1]);
         }
       }
+#endif
       tk = __builtin_readcyclecounter();  // the histogram's own time is left out
+#endif
+#ifdef FS_PHASE_PROF
+      act[0] += (uint64_t)__popcll(__ballot(1));
+      act[1] += (uint64_t)__popcll(__ballot(!(SUSP && parked) && h.obj >= 0));
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, TEX, SUSP, SOCT>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small, &parked);
+      scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
+                                                        &parked);
 #endif
       FS_PHASE(2);
       if (SUSP && parked) {
@@ -1754,9 +1864,11 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
+#ifndef FS_MEAS_NO_LVL  // measurement builds only (tools/gpu_writes.sh): the write streams one by one
         *at_byte(reinterpret_cast<float*>(lvl), (depth * kBlock + lane) * 4u) = c;  // [level][lane]
         if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)  // [kMaxDepth + level][lane]
           *at_byte(reinterpret_cast<float*>(lvl), ((kMaxDepth + depth) * kBlock + lane) * 4u) = ds;
+#endif
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0 && kind == FS_MAT_FOG) {  // Fog draws with the distance of its two anchors
@@ -1787,6 +1899,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       }
     }
     FS_PHASE(3);
+#ifdef FS_PHASE_PROF
+    act[2] += (uint64_t)__popcll(__ballot(done));
+    if (done) act[3] += (uint64_t)(top + 1);
+#endif
     if (done) {
       f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
       if (slot & kFog0) {  // both anchors were written (a Fog hit always bounces on to depth 1)
@@ -1795,11 +1911,19 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         lp0 = mk3(b.x, b.y, b.z);
       }
       L = unwind<TEX, MMAT, !SUSP>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);  // [channel][sample][pixel]
+      float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);
       const uint32_t o = slot & ~(0x80000000u | kFog0);
+#ifndef FS_MEAS_NO_RAD
+#if FS_RAD_XYZ  // [sample][pixel][channel]: one 12-B store per sample
+      store_rgb(rad + 3 * o, L);
+#else  // [channel][sample][pixel]
       rad[o] = L.x;
       rad[P.spp * kBlock + o] = L.y;
       rad[2 * P.spp * kBlock + o] = L.z;
+#endif
+#else
+      if (L.x == 1234.5f) rad[o] = L.y;  // keeps L live
+#endif
       if (COUNT) samples_done++;
       fresh = true;
     }
@@ -1810,8 +1934,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   }
 #ifdef FS_PHASE_PROF
   ph[9] = __builtin_readcyclecounter() - t_begin;
-  if (lane == 0)
+  if (lane == 0) {
     for (int i = 0; i < 10; i++) atomicAdd(&counters->phase[i], (unsigned long long)ph[i]);
+    atomicAdd(&counters->phase[14], (unsigned long long)ph[10]);
+    for (int i = 0; i < 3; i++) atomicAdd(&counters->phase[26 + i], (unsigned long long)act[i]);
+  }
+  atomicAdd(&counters->phase[29], (unsigned long long)act[3]);
   atomicAdd(&counters->phase[10], (unsigned long long)tally.node_trips);
   atomicAdd(&counters->phase[11], (unsigned long long)tally.leaf_trips);
   atomicAdd(&counters->phase[12], (unsigned long long)tally.lane_nodes);
@@ -1826,6 +1954,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     atomicAdd(&counters->prim_tests, (unsigned long long)tally.prims);
     atomicAdd(&counters->object_loads, (unsigned long long)tally.objs);
     atomicAdd(&counters->small_tri_loads, (unsigned long long)tally.utris);
+    atomicAdd(&counters->lane_object_loads, (unsigned long long)tally.lane_objs);
   }
 }
 
@@ -1850,7 +1979,11 @@ __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, cons
     const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * P.spp * kBlock);
     for (uint32_t k = 0; k < P.spp; k++) {
       const uint32_t o = k * kBlock + lane;
+#if FS_RAD_XYZ
+      f3 L = mk3(rad[3 * o], rad[3 * o + 1], rad[3 * o + 2]);
+#else
       f3 L = mk3(rad[o], rad[P.spp * kBlock + o], rad[2 * P.spp * kBlock + o]);
+#endif
       f3 np = mean * (float)n + L;
       float dv = (float)(++n);
       mean = mk3(np.x / dv, np.y / dv, np.z / dv);
@@ -2005,6 +2138,7 @@ struct fs_context {
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
   bool has_parking = false;  // a mesh of >= park_min_tris triangles: the PARKED schedule
+  bool has_walks = false;    // a mesh with a BVH (not small): the kernel needs the walk stack
   bool many_materials = false;  // > kPackedMaterials: material ids in scratch rows (MMAT kernels)
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
   std::vector<uint32_t> tile_order_host;  // the device tile_order buffer holds this order of ...
@@ -2112,9 +2246,12 @@ int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, uint32
               bool mat_rows) {
   const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + (mat_rows ? 4 * kMaxDepth : 0);
   const size_t bytes = (size_t)wave_lanes * per + (size_t)block_lanes * 12 * spp + 5 * 256;  // + alignment
+  // Shrink a buffer more than 4x (and 1 GiB) larger than this render needs:
+  // a context that once rendered a long launch does not keep its rows.
+  if (ctx->rows.bytes > 4 * bytes && ctx->rows.bytes - bytes > (1ull << 30)) ctx->rows.release();
   if (ctx->rows.bytes < bytes) {
     int rc = ensure(&ctx->rows, bytes);
-    if (rc) return rc;
+    if (rc) return rc == FS_ERR_DEVICE ? fail(FS_ERR_NOMEM, "scratch rows: " + g_error) : rc;
   }
   char* p = (char*)ctx->rows.p;
   auto take = [&](size_t n) {
@@ -2191,6 +2328,11 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #ifndef FS_SUSP_WAVES
 #define FS_SUSP_WAVES 6
 #endif
+// Waves per SIMD of the NOWALK kernel (no LDS stack: the LDS rows take 4 KiB
+// per wave, so up to 8 waves fit).
+#ifndef FS_NOWALK_WAVES
+#define FS_NOWALK_WAVES 6
+#endif
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
 
@@ -2204,22 +2346,28 @@ struct LeanKernel {
   const char* name;
   uint32_t waves;  // waves per SIMD (__launch_bounds__)
 };
-template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false>
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false>
 LeanKernel lean_kernel(bool count) {
-  constexpr int W = SUSP ? FS_SUSP_WAVES : FS_LEAN_WAVES;
+  constexpr int W = SUSP ? FS_SUSP_WAVES : NOWALK ? FS_NOWALK_WAVES : FS_LEAN_WAVES;
   static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
                                   (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
-                                  (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ">";
-  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT>
-                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT>,
+                                  (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") +
+                                  (NOWALK ? ", true>" : ", false>");
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK>,
           name.c_str(), (uint32_t)W};
 }
 // Scenes traced through the object octree take one instantiation that covers
 // textures and any material count (their object loop is per lane anyway).
-LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree) {
+// Untextured scenes whose meshes are all small (no BVH walk) take the NOWALK
+// instantiation: no walk stack, shading rows in LDS.
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks) {
   if (object_tree) return lean_kernel<true, false, true, true>(count);
   if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
   if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
+  if (!walks)
+    return many_materials ? lean_kernel<false, false, true, false, true>(count)
+                          : lean_kernel<false, false, false, false, true>(count);
   return many_materials ? lean_kernel<false, false, true>(count) : lean_kernel<false, false, false>(count);
 }
 
@@ -2232,6 +2380,9 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->node_layout > FS_NODE_LAYOUT_PAIRS) *why = "unknown node_layout";
   else if (o->persist > 1) *why = "persist must be 0 or 1";
   else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
+  else if (o->park_lanes > 64 || o->park_lanes_small > 64) *why = "park_lanes must be 0..64";
+  else if (o->park_entry > 64 || o->park_entry_small > 64) *why = "park_entry must be 0..64";
+  else if (o->lds_rows > 1) *why = "lds_rows must be 0 or 1";
   else return true;
   return false;
 }
@@ -2300,6 +2451,7 @@ int fs_options_default(fs_options* o) {
   o->park_lanes = 10;       // C4 (1 M-face blob): 10-12 best
   o->park_lanes_small = 6;  // C3 (38 k and 209 k-face meshes): 4-6 best
   o->park_min_tris = kParkMinTris;
+  o->lds_rows = 1;
   o->samples_per_block = 16;  // persistent waves: C4 +0.7 %, C3 +2 %, C2 +3 % over 64 (8 and 4 no better)
   o->groups = 0;
   o->group_major = 0;
@@ -2427,7 +2579,11 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   ctx->has_textures = false;
   for (const fs_material& m : P.materials) ctx->has_textures |= m.texture >= 0;
   ctx->has_parking = false;
-  for (const DevObject& o : P.objects) ctx->has_parking |= o.kind == FS_OBJ_MESH && o.i5 != 0;
+  ctx->has_walks = false;
+  for (const DevObject& o : P.objects) {
+    ctx->has_parking |= o.kind == FS_OBJ_MESH && o.i5 != 0;
+    ctx->has_walks |= o.kind == FS_OBJ_MESH && o.i2 && !o.i3;
+  }
   ctx->many_materials = P.materials.size() > kPackedMaterials;
   ctx->num_objects = S.num_objects;
   ctx->host = std::move(P);
@@ -2536,8 +2692,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_stride = stride;
   L.seed = params->seed;
   const fs_options& O = ctx->opt;
-  L.susp_thr = O.park_lanes;
-  L.susp_thr_small = O.park_lanes_small;
+  L.susp_thr = O.park_lanes | (O.park_entry << 8);
+  L.susp_thr_small = O.park_lanes_small | (O.park_entry_small << 8);
   // XCD placement: 0 dispatch order, 1 one band per XCD (C4 -25 %: the bands
   // are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
   L.xcd_bands = O.xcd_bands;
@@ -2571,9 +2727,19 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // >= kGroupTargetBlocks blocks (about 43 per wave slot of the chip).
   const uint32_t full_chunks = params->spp / chunk;
   uint32_t G = 1;
+  // The radiance rows of a persistent launch: at most kRadianceRowBytes and at
+  // most half of the device memory that is free (counting the rows this
+  // context already holds), so a smaller or shared GPU renders in more,
+  // smaller launches instead of failing.
+  uint64_t row_budget = kRadianceRowBytes;
+  {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      row_budget = std::min<uint64_t>(row_budget, (free_b + ctx->rows.bytes) / 2);
+  }
   if (blocks && full_chunks > 1) {
     uint64_t want = O.groups  ? (uint64_t)O.groups
-                    : O.persist ? std::max<uint64_t>(1, kRadianceRowBytes / (blocks * 12ull * chunk * kBlock))
+                    : O.persist ? std::max<uint64_t>(1, row_budget / (blocks * 12ull * chunk * kBlock))
                                 : (kGroupTargetBlocks + blocks - 1) / blocks;
     want = std::max<uint64_t>(1, std::min<uint64_t>({want, full_chunks, ((1ull << 31) - 1) / blocks}));
     const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
@@ -2614,14 +2780,20 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   LeanRows rows;
   const bool tree = ctx->scene.tree != nullptr;
   const bool mm = ctx->many_materials || tree;
-  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr);
+  const LeanKernel K =
+      pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr, ctx->has_walks || !O.lds_rows);
   // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
   // K.waves waves per SIMD), never more than the launch has blocks.
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
   const uint64_t max_grid = O.persist ? std::min<uint64_t>(wave_slots, blocks * G) : blocks * G;
   if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
-  if (blocks && (rc = lean_rows(ctx, max_grid * kBlock, blocks * G * kBlock, chunk, &rows, ctx->has_textures || tree, mm)))
-    return rc;
+  // On an allocation failure the launches shrink (G halved) until the rows fit.
+  while (blocks && (rc = lean_rows(ctx, std::min<uint64_t>(max_grid, blocks * G) * kBlock, blocks * G * kBlock, chunk,
+                                   &rows, ctx->has_textures || tree, mm))) {
+    if (G == 1 || O.groups) return rc;
+    G = (G + 1) / 2;
+    (void)hipGetLastError();  // clear the failed hipMalloc's error state
+  }
   ctx->last_kernel = K.name;
   L.persist = O.persist;
   for (uint32_t done = 0; done < params->spp && blocks;) {
@@ -2684,6 +2856,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->prim_tests = c.prim_tests;
   out->object_loads = c.object_loads;
   out->small_tri_loads = c.small_tri_loads;
+  out->lane_object_loads = c.lane_object_loads;
 #ifdef FS_PHASE_PROF
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "
@@ -2695,6 +2868,12 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                "trips, %llu lane leaves (%.1f%%)\n",
                c.phase[10], c.phase[12], 100.0 * c.phase[12] / (64.0 * (c.phase[10] ? c.phase[10] : 1)), c.phase[11],
                c.phase[13], 100.0 * c.phase[13] / (64.0 * (c.phase[11] ? c.phase[11] : 1)));
+  std::fprintf(stderr,
+               "[fs small] small-mesh faces %llu cycles (inside mesh-traversal); lanes per iteration: tracing %.1f, "
+               "shading %.1f, finishing %.1f; unwind levels per finished path %.2f\n",
+               c.phase[14], (double)c.phase[26] / (c.phase[8] ? c.phase[8] : 1),
+               (double)c.phase[27] / (c.phase[8] ? c.phase[8] : 1), (double)c.phase[28] / (c.phase[8] ? c.phase[8] : 1),
+               (double)c.phase[29] / (c.phase[28] ? c.phase[28] : 1));
   std::fprintf(stderr, "[fs hist] node visits per segment: 0:%llu 1-4:%llu 5-8:%llu 9-16:%llu 17-32:%llu 33-64:%llu "
                "65-128:%llu >128:%llu\n", c.phase[16], c.phase[17], c.phase[18], c.phase[19], c.phase[20],
                c.phase[21], c.phase[22], c.phase[23]);
@@ -2742,6 +2921,12 @@ int fs_prepare_digest(const fs_scene_desc* desc, const fs_options* opt, uint64_t
   mix(P.tri_tex.data(), P.tri_tex.size() * sizeof(float));
   mix(P.materials.data(), P.materials.size() * sizeof(fs_material));
   mix(P.tex_rgb.data(), P.tex_rgb.size() * sizeof(float));
+  mix(P.tex_info.data(), P.tex_info.size() * sizeof(uint32_t));
+  mix(P.table.data(), P.table.size() * sizeof(float));
+  if (P.tree_valid) {  // the object octree of an optimised scene (SceneBvh)
+    mix(&P.tree, sizeof(P.tree));
+    mix(P.tree_objs.data(), P.tree_objs.size() * sizeof(uint32_t));
+  }
   *digest = h;
   if (num_nodes) *num_nodes = P.nodes.size();
   if (build_ms) *build_ms = P.build_ms;
@@ -2797,6 +2982,14 @@ int fs_comm_init(fs_context* ctx, int nranks, int rank, const uint8_t id[FS_COMM
   if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   ctx->nranks = nranks;
   ctx->rank = rank;
+  return FS_OK;
+}
+
+int fs_comm_count(fs_context* ctx, int* count) {
+  if (!ctx || !count) return fail(FS_ERR_INVALID, "null argument");
+  if (!ctx->comm) return fail(FS_ERR_STATE, "fs_comm_count before fs_comm_init");
+  ncclResult_t r = ncclCommCount(ctx->comm, count);
+  if (r != ncclSuccess) return fail(FS_ERR_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(r));
   return FS_OK;
 }
 

@@ -71,7 +71,8 @@ struct DevFrame {
 };
 
 struct DevCounters {
-  unsigned long long samples, segments, node_visits, tri_tests, prim_tests, object_loads, small_tri_loads;
+  unsigned long long samples, segments, node_visits, tri_tests, prim_tests, object_loads, small_tri_loads,
+      lane_object_loads;
   // Per-wave cycle totals by loop phase; filled only by -DFS_PHASE_PROF
   // builds (libfsgpu_prof.so, a measurement tool, never the product path).
   unsigned long long phase[32];

@@ -88,7 +88,7 @@ class fs_render_params(C.Structure):
 class fs_counters(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("prim_tests", C.c_uint64), ("object_loads", C.c_uint64),
-                ("small_tri_loads", C.c_uint64)]
+                ("small_tri_loads", C.c_uint64), ("lane_object_loads", C.c_uint64)]
 
 
 class fs_options(C.Structure):
@@ -97,7 +97,9 @@ class fs_options(C.Structure):
                 ("tile_order", C.c_uint32), ("xcd_bands", C.c_uint32), ("gpu_bvh_min_tris", C.c_uint32),
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
-                ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32)]
+                ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
+                ("park_entry", C.c_uint32), ("park_entry_small", C.c_uint32),
+                ("lds_rows", C.c_uint32)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
@@ -133,6 +135,7 @@ GPU_SYMBOLS = {
     "fs_comm_unique_id": ([C.c_char_p], C.c_int),
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
+    "fs_comm_count": ([_VP, C.POINTER(C.c_int)], C.c_int),
     "fs_comm_destroy": ([_VP], C.c_int),
     "fs_frame_pack_bytes": ([C.POINTER(fs_render_params), C.POINTER(C.c_uint64)], C.c_int),
     "fs_frame_pack": ([_VP, _VP, C.POINTER(fs_render_params), _VP, C.c_size_t], C.c_int),
@@ -491,6 +494,11 @@ class Renderer:
 
     def comm_init(self, nranks, rank, uid):
         _check(gpu_lib().fs_comm_init(self.ctx, nranks, rank, uid), "fs_comm_init")
+
+    def comm_count(self):
+        n = C.c_int()
+        _check(gpu_lib().fs_comm_count(self.ctx, C.byref(n)), "fs_comm_count")
+        return n.value
 
     def gather(self, frame, params, root=0):
         _check(gpu_lib().fs_frame_gather(self.ctx, frame.h, C.byref(params), root), "fs_frame_gather")

@@ -328,6 +328,29 @@ fs_object QuadObject::Describe() const {
 // Restates the parts of the vendored tinyobj loader (tiny_obj_loader.h) that
 // decide the triangles MeshObject sees: its number parser, index fixing and
 // the ear-clipping triangulation of polygons.
+//
+// try_parse_double, pnpoly and triangulate_face below are derived from
+// tinyobjloader v1.2.2 (the copy vendored by the reference), which carries
+// this notice:
+//
+//   The MIT License (MIT)
+//   Copyright (c) 2012-2018 Syoyo Fujita and many contributors.
+//   Permission is hereby granted, free of charge, to any person obtaining a
+//   copy of this software and associated documentation files (the
+//   "Software"), to deal in the Software without restriction, including
+//   without limitation the rights to use, copy, modify, merge, publish,
+//   distribute, sublicense, and/or sell copies of the Software, and to permit
+//   persons to whom the Software is furnished to do so, subject to the
+//   following conditions:
+//   The above copyright notice and this permission notice shall be included
+//   in all copies or substantial portions of the Software.
+//   THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS
+//   OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF
+//   MERCHANTABILITY, FITNESS FOR A PARTICULAR PURPOSE AND NONINFRINGEMENT. IN
+//   NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM,
+//   DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR
+//   OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE
+//   USE OR OTHER DEALINGS IN THE SOFTWARE.
 namespace {
 
 // tryParseDouble (tiny_obj_loader.h:537-650): digits accumulated in double,

@@ -218,6 +218,35 @@ int type_size(int t) { return t == kHalf ? 2 : 4; }
 // and their error points, and, as tinyexr does, the decoder's failures
 // are not fatal: the buffer keeps what was decoded (DecompressPiz only
 // fails on a bad bitmap range).
+//
+// The decoder below (wav2_decode in particular) is derived from tinyexr,
+// which carries OpenEXR's PIZ code; both notices apply:
+//
+//   Copyright (c) 2014 - 2018, Syoyo Fujita and many contributors.
+//   Copyright (c) 2002, Industrial Light & Magic, a division of Lucas
+//   Digital Ltd. LLC. All rights reserved.
+//   Redistribution and use in source and binary forms, with or without
+//   modification, are permitted provided that the following conditions are
+//   met:
+//   * Redistributions of source code must retain the above copyright
+//     notice, this list of conditions and the following disclaimer.
+//   * Redistributions in binary form must reproduce the above copyright
+//     notice, this list of conditions and the following disclaimer in the
+//     documentation and/or other materials provided with the distribution.
+//   * Neither the name of Syoyo Fujita / Industrial Light & Magic nor the
+//     names of its contributors may be used to endorse or promote products
+//     derived from this software without specific prior written permission.
+//   THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND CONTRIBUTORS "AS
+//   IS" AND ANY EXPRESS OR IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO,
+//   THE IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR A PARTICULAR
+//   PURPOSE ARE DISCLAIMED. IN NO EVENT SHALL THE COPYRIGHT OWNER OR
+//   CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL,
+//   EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO,
+//   PROCUREMENT OF SUBSTITUTE GOODS OR SERVICES; LOSS OF USE, DATA, OR
+//   PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED AND ON ANY THEORY OF
+//   LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING
+//   NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS
+//   SOFTWARE, EVEN IF ADVISED OF THE POSSIBILITY OF SUCH DAMAGE.
 namespace piz {
 constexpr int kEncSize = (1 << 16) + 1;  // HUF_ENCSIZE
 constexpr int kDecBits = 14, kDecSize = 1 << kDecBits, kDecMask = kDecSize - 1;

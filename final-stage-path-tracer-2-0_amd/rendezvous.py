@@ -10,8 +10,10 @@ so the bench's GPU processes never import torch.
 
 All ranks must be on one host (the directory is local). The directory name
 is derived from the launcher's environment (MASTER_PORT, TORCHELASTIC_RUN_ID,
-the restart count) and the parent process id, which every worker of one
-torchrun agent shares.
+the restart count), the parent process id, which every worker of one
+torchrun agent shares, and that parent's start time (a per-launch nonce: a
+reused pid, or a rerun with the same port and run id, gets a fresh
+directory, so no rank can read files a failed earlier launch left behind).
 """
 from __future__ import annotations
 
@@ -22,9 +24,21 @@ import tempfile
 import time
 
 
+def _start_time(pid: int) -> str:
+    """Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat
+    field 22), or "0" where /proc is unavailable."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            stat = f.read()
+        return stat[stat.rindex(")") + 2:].split()[19]
+    except (OSError, ValueError, IndexError):
+        return "0"
+
+
 def default_dir() -> str:
+    ppid = os.getppid()
     key = "_".join([os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "none"),
-                    os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"), str(os.getppid())])
+                    os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"), str(ppid), _start_time(ppid)])
     return os.path.join(tempfile.gettempdir(), f"fs_rdzv_{os.getuid()}_{key}")
 
 
@@ -36,7 +50,8 @@ class FileGroup:
     for a rank when the files it waits for exist. The files of operation k
     are deleted once operation k + 1 has completed (every rank has then left
     k); close() ends with a "done" file per rank, after which rank 0 removes
-    the directory.
+    the directory. abort() (a rank that fails) removes the rank's own files,
+    and rank 0's removes the directory.
     """
 
     def __init__(self, rank: int, world: int, path: str | None = None, timeout: float = 900.0,
@@ -100,12 +115,16 @@ class FileGroup:
         self._done(seq)
 
     def broadcast(self, data: bytes | None, root: int = 0) -> bytes:
-        """root's bytes on every rank (others pass None)."""
+        """root's bytes on every rank (others pass None; only the root writes
+        a file)."""
         if self.rank == root and data is None:
             raise ValueError("the root must pass the data")
         seq = self.seq
-        got = self._op(data if self.rank == root else b"", [root])
-        self.barrier()  # everyone has read the root's file (and drops its own file `seq`)
+        self.seq += 1
+        if self.rank == root:
+            self._put(seq, data)
+        got = self._wait(seq, [root])
+        self.barrier()  # everyone has read the root's file (the root drops it)
         return got[root]
 
     def max(self, value: float) -> float:
@@ -113,6 +132,29 @@ class FileGroup:
         got = self._op(struct.pack("<d", float(value)), range(self.world))
         self._done(seq)
         return max(struct.unpack("<d", v)[0] for v in got.values())
+
+    def allgather(self, values) -> list:
+        """Every rank's list of floats (all of one length), in rank order."""
+        vals = [float(v) for v in values]
+        seq = self.seq
+        got = self._op(struct.pack(f"<{len(vals)}d", *vals), range(self.world))
+        self._done(seq)
+        return [list(struct.unpack(f"<{len(got[r]) // 8}d", got[r])) for r in range(self.world)]
+
+    def abort(self) -> None:
+        """Clean-up of a rank that fails: its own files go; rank 0 removes the
+        directory (other ranks then time out instead of reading stale files)."""
+        try:
+            for name in os.listdir(self.path):
+                if name.split(".")[1:2] == [str(self.rank)]:
+                    try:
+                        os.remove(os.path.join(self.path, name))
+                    except FileNotFoundError:
+                        pass
+        except OSError:
+            pass
+        if self.rank == 0:
+            shutil.rmtree(self.path, ignore_errors=True)
 
     def close(self) -> None:
         """Every rank writes its "done" file after its last read; rank 0 waits

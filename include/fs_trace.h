@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 4
+#define FS_ABI_VERSION 5
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -212,6 +212,9 @@ typedef struct fs_counters {
   uint64_t small_tri_loads; /* triangle records of small meshes (fs_options.small_mesh_tris),
                                wave-uniform loads, once per wave; their per-lane tests are
                                not in tri_tests */
+  uint64_t lane_object_loads; /* object records read at a per-lane index (the object
+                                  octree of an optimised scene, scene.cpp:216-236): vector
+                                  loads, once per lane */
 } fs_counters;
 
 typedef struct fs_context fs_context;
@@ -239,7 +242,12 @@ typedef struct fs_options {
                                   >= 2^19 triangles (10) */
   uint32_t park_min_tris;      /* meshes whose walks may park (32768); read at upload */
   uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (16) */
-  uint32_t groups;             /* sample groups per launch; 0 = sized to >= 262144 blocks (0) */
+  uint32_t groups;             /* sample groups per launch (0). 0 = automatic: with persist = 1
+                                  as many groups as a radiance-row budget allows (12 B per
+                                  sample of a launch, at most 32 GiB and at most half the free
+                                  device memory: C4 at 1080p x 1024 spp is one launch with
+                                  25.5 GB of rows); with persist = 0 enough groups for
+                                  >= 262144 blocks per launch */
   uint32_t group_major;        /* block order: 0 a tile's groups together (0), 1 group by group */
   uint32_t tile_order;         /* 1 centre-first dispatch of owned tiles (1), 0 index order */
   uint32_t xcd_bands;          /* 2 whole 64x64 tiles per XCD (2), 1 one band per XCD, 0 none */
@@ -256,6 +264,12 @@ typedef struct fs_options {
                                   face by face with wave-uniform loads, no BVH walk (16; 0 off,
                                   max 64); read at upload */
   uint32_t park_lanes_small;   /* PARKED: park_lanes for parkable meshes under 2^19 triangles (6) */
+  uint32_t park_entry;         /* PARKED: a walk of a mesh of >= 2^19 triangles starts only when at
+                                  least this many lanes want it (or no other lane can go on);
+                                  the others wait parked at the root (0 = off; 0..64) */
+  uint32_t park_entry_small;   /* the same for the smaller parkable meshes (0 = off; 0..64) */
+  uint32_t lds_rows;           /* 1: scenes without BVH walks (every mesh small, no texture) run
+                                  the NOWALK kernel, shading rows in LDS (1); 0 the LEAN kernel */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */
@@ -322,6 +336,10 @@ int fs_comm_init(fs_context* ctx, int nranks, int rank,
 /* Gathers every rank's owned tiles (per params' tiling) into root's frame. */
 int fs_frame_gather(fs_context* ctx, fs_frame* frame,
                     const fs_render_params* params, int root);
+/* Ranks of the context's RCCL communicator (ncclCommCount); FS_ERR_STATE
+ * before fs_comm_init. Lets a multi-GPU bench line state how many ranks the
+ * gather really spanned. */
+int fs_comm_count(fs_context* ctx, int* count);
 int fs_comm_destroy(fs_context* ctx);
 
 /* The tile exchange of fs_frame_gather without RCCL, through host memory

@@ -563,6 +563,7 @@ OPTION_VARIANTS = [
     {"schedule": "parked", "park_min_tris": 1},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63, "park_lanes_small": 63},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes_small": 1},
+    {"schedule": "parked", "park_min_tris": 1, "park_entry": 48, "park_entry_small": 64},
     {"samples_per_block": 64},
     {"samples_per_block": 7},
     {"xcd_bands": 0},
@@ -576,6 +577,7 @@ OPTION_VARIANTS = [
     {"persist": 0, "samples_per_block": 7, "groups": 3},
     {"small_mesh_tris": 0},
     {"small_mesh_tris": 64},
+    {"lds_rows": 0},
 ]
 
 

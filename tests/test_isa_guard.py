@@ -1,0 +1,51 @@
+"""ISA regression guard (CPU): the product trace kernels' scratch, register
+spills and VGPR budget, read from the gfx950 code object in libfsgpu.so.
+
+Several of the kernel's measured gains rest on how the compiler allocates
+registers (cold records read at their use, the integer-min
+slab clamp, the 6-wave launch bound); every 8-16 B/lane of extra spills has
+cost 1-2 %. A toolchain update or a source change that undoes them fails
+here before it reaches a GPU. Raising a limit is a deliberate edit, made
+with the A/B that justifies it."""
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import isa_guard  # noqa: E402
+
+# kernel (as fs_last_kernel names it) -> (max scratch B/lane, max SGPR spills, VGPRs)
+LIMITS = {
+    # PARKED schedule: C3 and C4 (the bench kernel)
+    "render_kernel_lean<false, 6, false, true, false, false, false>": (44, 21, 80),
+    # LEAN schedule: scenes with BVH walks and no large mesh
+    "render_kernel_lean<false, 6, false, false, false, false, false>": (16, 10, 80),
+    # LEAN without walks (NOWALK: every mesh small, shading rows in LDS): C1 and C2
+    "render_kernel_lean<false, 6, false, false, false, false, true>": (0, 8, 80),
+}
+
+
+@pytest.fixture(scope="module")
+def resources():
+    if not os.path.exists(isa_guard.READELF):
+        pytest.skip("llvm-readelf not in this image")
+    return {isa_guard.demangle_lean(k): v for k, v in isa_guard.kernel_resources().items()
+            if isa_guard.demangle_lean(k)}
+
+
+@pytest.mark.parametrize("kernel", sorted(LIMITS))
+def test_trace_kernel_spills_within_budget(kernel, resources):
+    assert kernel in resources, f"{kernel} not in libfsgpu.so"
+    r = resources[kernel]
+    scratch, sgpr_spills, vgprs = LIMITS[kernel]
+    assert r["private_segment_fixed_size"] <= scratch, r
+    assert r["sgpr_spill_count"] <= sgpr_spills, r
+    assert r["vgpr_count"] <= vgprs, r  # 6 waves per SIMD (512 / 80)
+
+
+def test_every_product_kernel_keeps_six_waves(resources):
+    for name, r in resources.items():
+        if name.startswith("render_kernel_lean<false"):
+            assert r["vgpr_count"] <= 80, (name, r)  # __launch_bounds__(64, 6)
+            assert r["group_segment_fixed_size"] <= 160 * 1024 // 24, (name, r)  # 24 waves' LDS per CU

@@ -11,10 +11,17 @@ import fsamd  # noqa: E402
 import oracle_py  # noqa: E402
 import scenes  # noqa: E402
 
-REF = {"c1": 0.73, "c3": 0.180, "c4": 0.067}  # SURVEY.md §8(d) [probe], Msamples/s on 8 threads
+REF = {"c1": 0.73, "p250": 0.180, "c3": 0.180, "c4": 0.067}  # SURVEY.md §8(d) [probe], Msamples/s on 8 threads
 threads = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-for name, W, H, spp, stride in (("c1", 256, 256, 8, 1), ("c3", 1920, 1080, 1, 8), ("c4", 1920, 1080, 1, 16)):
-    p = scenes.write(name, f"/tmp/fs_calib/{name}")
+which = sys.argv[2].split(",") if len(sys.argv) > 2 else ["c1", "p250", "c3", "c4"]
+for name, W, H, spp, stride in (("c1", 256, 256, 8, 1), ("p250", 1920, 1080, 1, 8), ("c3", 1920, 1080, 1, 8),
+                                ("c4", 1920, 1080, 1, 16)):
+    if name not in which:
+        continue
+    if name == "p250":
+        p = scenes.write_c4(f"/tmp/fs_calib/{name}", nu=500, nv=250)
+    else:
+        p = scenes.write(name, f"/tmp/fs_calib/{name}")
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()
