@@ -700,7 +700,7 @@ def test_many_materials_bit_exact(variant, gpu_renderer):
         gpu_renderer.set_options(schedule="parked", park_min_tris=1)
     out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
     k = gpu_renderer.last_kernel()
-    assert k[:-1].split(", ")[4] == "true", k  # the MMAT instantiation <.., TEX, SUSP, MMAT, SOCT>
+    assert k[:-1].split(", ")[4] == "true", k  # the MMAT instantiation <.., TEX, SUSP, MMAT, SOCT, NOWALK>
     assert (k[:-1].split(", ")[3] == "true") == (variant == "parked"), k
     ref = oracle_render(ptr, CAM, 96, 72, 16)
     assert_parity(out, ref, exact=True)
@@ -767,7 +767,7 @@ def test_object_octree_scene_bit_exact(optimized, gpu_renderer):
     cam = fsamd.camera((0, 10, -34), (0, 10, 0), fov_y=40, aperture=0.0)
     out = gpu_render(gpu_renderer, ptr, cam, 96, 72, 16)
     k = gpu_renderer.last_kernel()
-    assert (k[:-1].split(", ")[-1] == "true") == optimized, k  # the object-octree instantiation
+    assert (k[:-1].split(", ")[5] == "true") == optimized, k  # the object-octree instantiation (SOCT)
     ref = oracle_render(ptr, cam, 96, 72, 16)
     assert_parity(out, ref, exact=True)
     _record("object_octree", {"optimized": optimized, "mean": float(out[fsamd.PLANE_COLOR].mean())})
@@ -797,7 +797,7 @@ def test_object_octree_loaded_scene_and_trace_range(tmp_path, gpu_renderer):
     assert s.desc().contents.flags & fsamd.SCENE_OPTIMIZED and s.desc().contents.num_objects == 190
     cam = s.camera(0)
     out = gpu_render(gpu_renderer, s, cam, 80, 60, 8)
-    assert gpu_renderer.last_kernel()[:-1].split(", ")[-1] == "true"
+    assert gpu_renderer.last_kernel()[:-1].split(", ")[5] == "true"  # SOCT
     ref = oracle_render(s.desc_ptr(), cam, 80, 60, 8)
     assert_parity(out, ref, exact=True)
     pts = np.random.default_rng(1).uniform([0, 0], [80, 60], (200, 2)).astype(np.float32)
