@@ -58,8 +58,10 @@ WORKLOADS = {
 S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
 # tools/cpu_calibration.py, survey container, 8 threads, against the reference rates
 # of SURVEY.md §6 [probe]
-CPU_CALIBRATION = ("restatement/reference rate 1.03 on C4 1080p (8 threads, survey container; DESIGN §6): "
-                   "the baseline stands for the reference on C4")
+CPU_CALIBRATION = ("restatement/reference rate on the survey's probe scenes (8 threads, build container, DESIGN "
+                   "§6): C1 0.99-1.18, 250k probe 0.55-0.64, C4 0.65-0.66 this session (C4 1.03 in round 2's): "
+                   "within a factor of about 2 either way; the reference cannot be built here for a same-machine "
+                   "calibration")
 
 
 def parse():
@@ -232,20 +234,24 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
     valu = None
     if pm and pm.get("hbm_bytes_per_sample"):
         traffic = round(pm["hbm_bytes_per_sample"] * owned_samples / launches)
-    if pm and pm.get("valu_insts_per_sample"):
-        # VALU against the gfx950 peak, replayed per sample from the PMC file onto this
-        # run's launch time: issue = wave64 VALU instructions x 2 cycles (32-lane SIMD,
-        # MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc) over the 1024 SIMDs' cycles at
-        # the clock the PMC run measured (GRBM_GUI_ACTIVE / 8 / launch time); lane-op rate =
-        # active lanes x instructions against 1024 SIMDs x 32 lanes x 2.4 GHz (= 157.3 TF / 2)
-        insts = pm["valu_insts_per_sample"] * owned_samples / launches
-        clock = pm.get("clock_ghz") or 2.4
-        issue_frac = insts * 2 / (1024 * clock * 1e9 * avg_launch_s)
+    if pm and pm.get("valu_insts_per_sample") and pm.get("clock_ghz"):
+        # VALU against the gfx950 peak, replayed per sample from the PMC file onto
+        # this run's launch time at the clock the PMC run measured (GRBM_GUI_ACTIVE
+        # / 8 / kernel time): issue = wave64 VALU instructions x 2 cycles (the
+        # FP32 rate, MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc) over the 1024
+        # SIMDs' cycles; lane-op rate = instructions x active lanes against 1024
+        # SIMDs x 32 lanes x 2.4 GHz (157.3 TF FP32 / 2 per FMA)
+        samples_launch = owned_samples / launches
+        clock = pm["clock_ghz"] * 1e9
+        insts = pm["valu_insts_per_sample"] * samples_launch
+        issue = insts * 2 / (1024 * clock * avg_launch_s)
         lane_ops = insts * 64 * pm["valu_lane_util"]
-        lane_frac = lane_ops / avg_launch_s / VALU_LANE_OPS_PEAK
-        valu = {"valu_busy": round(issue_frac, 4), "valu_lane_util": pm["valu_lane_util"],
-                "valu_lane_op_frac": round(lane_frac, 4), "clock_ghz": clock,
-                "wait_any_frac": pm.get("wait_any_frac")}
+        valu = {"valu_issue_frac": round(issue, 4), "valu_busy_rocprof": pm.get("valu_busy"),
+                "valu_lane_util": pm["valu_lane_util"],
+                "valu_lane_op_frac": round(lane_ops / avg_launch_s / VALU_LANE_OPS_PEAK, 4),
+                "valu_insts_per_sample": pm["valu_insts_per_sample"], "clock_ghz": pm["clock_ghz"],
+                "wait_any_frac": pm.get("wait_any_frac"),
+                "source": pm_path + " (replayed per sample, not measured by this run)"}
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(hbm_frac, 4), "traffic": traffic,
             "traffic_source": pm_path + " (replayed per sample, not measured by this run)" if traffic else None,
@@ -262,8 +268,8 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
             "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
             "small_tri_loads_per_sample": round(c["small_tri_loads"] / max(c["samples"], 1), 3),
             "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
-    if valu and valu["valu_busy"] > hbm_frac:
-        roof["bound"] = "valu"  # the larger of the two fractions names the binding resource
+    if valu and valu["valu_issue_frac"] > hbm_frac:
+        roof["bound"] = "valu"  # the larger of the two fractions names the nearer resource
     return roof
 
 

@@ -54,6 +54,10 @@
 // rows are written once, by lanes that finish in different iterations, so
 // their lines leave L2 partly written: measured write traffic 50 B per 12-B
 // sample with the planar layout.
+// POOL kernel: the shading waves' per-bounce rows in LDS (1) or HBM (0, A/B)
+#ifndef FS_POOL_LDS_ROWS
+#define FS_POOL_LDS_ROWS 1
+#endif
 #ifndef FS_RAD_XYZ
 #define FS_RAD_XYZ 1
 #endif
@@ -975,6 +979,193 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   return SUSP && susp;
 }
 
+// ---- the walk pool (POOL schedule) -----------------------------------------
+// A workgroup of kPoolWaves waves: wave 0 walks BVHs for the others, which
+// run everything else (tasks, the object loop, shading, the backward pass).
+// A lane that reaches a mesh with a BVH writes its segment into its own slot
+// of the workgroup's LDS pool and waits; the walk wave keeps its 64 lanes
+// busy with the pending walks of all three waves (refilling lanes as walks
+// finish), and posts each result back into the slot. The walk's operations
+// are those of traverse_ww, only on another lane: frames are identical.
+// Measured: the node loop ran 27 % of its lanes per trip in
+// the walking wave itself, and the kernel is VALU-issue bound.
+constexpr uint32_t kPoolWaves = 4;                       // 1 walk wave + 3 shading waves
+constexpr uint32_t kPoolSlots = (kPoolWaves - 1) * kBlock;
+constexpr uint32_t kPoolNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kPoolZl = 0x80000000u;                // root word bit: zero-length segment
+struct WalkPool {
+  // per slot (SoA): segment start, dir, the best t so far, root node | kPoolZl;
+  // after the walk the same words hold the result: t, u, v, prim (kPoolNoSlot: none), point
+  float f[8][kPoolSlots];
+  unsigned long long pending[kPoolWaves - 1];  // slots waiting for a walk (set by shaders, cleared by the walker)
+  unsigned long long done[kPoolWaves - 1];     // results posted (set by the walker, cleared by shaders)
+  uint32_t alive;                              // shading waves still running
+};
+
+__device__ __forceinline__ unsigned long long lds_load64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// position of the n-th (0-based) set bit of m (n < popcount(m))
+__device__ __forceinline__ uint32_t nth_set_bit(unsigned long long m, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t half = 32; half; half >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << half) - 1ull));
+    if (n >= c) {
+      n -= c;
+      m >>= half;
+      pos += half;
+    }
+  }
+  return pos;
+}
+
+// The walk wave. Lanes hold one pool slot's walk each; after every pass
+// (inner nodes until each lane holds a leaf, or until at most `refill`
+// lanes still walk while slots are pending; then the parked leaves) finished
+// lanes post their results and free lanes take pending slots, oldest wave
+// first in turn. Exits once every shading wave has exited (their waits all
+// ended) and no slot is pending.
+template <bool COUNT>
+__device__ void walk_service(const DevScene& S, WalkPool& pool, uint32_t* __restrict__ stk, uint32_t refill,
+                             Tally<COUNT>& tally) {
+  constexpr uint32_t kNone = 0x7FFFFFFFu;
+  const uint32_t lane = threadIdx.x & (kBlock - 1);
+  uint32_t slot = kPoolNoSlot;
+  uint32_t w = kNone, leaf = 0, sp = 0;
+  float tmax_lim = 0.0f;
+  bool zl = false;
+  Ray r;
+  Slopes sl{};
+  MinHit h;
+  h.t = 2.0f;
+  h.obj = -1;
+  uint32_t turn = 0;
+  for (;;) {
+    // 1. post finished walks
+    const bool fin = slot != kPoolNoSlot && w == kNone && leaf == 0;
+    if (fin) {
+      pool.f[0][slot] = h.t;
+      pool.f[1][slot] = h.u;
+      pool.f[2][slot] = h.v;
+      pool.f[3][slot] = __uint_as_float(h.obj >= 0 ? h.prim : kPoolNoSlot);
+      pool.f[4][slot] = __uint_as_float(h.point);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_fetch_or(&pool.done[slot >> 6], 1ull << (slot & 63), __ATOMIC_RELEASE,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      slot = kPoolNoSlot;
+    }
+    // 2. free lanes take pending slots
+    const unsigned long long freem = __ballot(slot == kPoolNoSlot);
+    uint32_t nfree = (uint32_t)__popcll(freem);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(freem >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)freem, 0u));
+    uint32_t base = 0;
+    bool any_pending = false;
+    for (uint32_t k = 0; k < kPoolWaves - 1; k++) {
+      const uint32_t sw = __builtin_amdgcn_readfirstlane((turn + k) % (kPoolWaves - 1));
+      unsigned long long pm = lds_load64(&pool.pending[sw]);
+      pm = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(pm >> 32)) << 32) |
+           (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pm);
+      if (!pm) continue;
+      if (!nfree) {
+        any_pending = true;
+        continue;
+      }
+      unsigned long long take = pm;
+      if ((uint32_t)__popcll(pm) > nfree) {  // the lowest nfree pending slots
+        const uint32_t cut = __builtin_amdgcn_readfirstlane(nth_set_bit(pm, nfree));
+        take = pm & ((1ull << cut) - 1ull);
+        any_pending = true;
+      }
+      const uint32_t nt = (uint32_t)__popcll(take);
+      if (lane == (uint32_t)__builtin_amdgcn_readfirstlane(lane))
+        __hip_atomic_fetch_and(&pool.pending[sw], ~take, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (slot == kPoolNoSlot && rank >= base && rank < base + nt) slot = sw * kBlock + nth_set_bit(take, rank - base);
+      base += nt;
+      nfree -= nt;
+    }
+    turn++;
+    const bool fresh = slot != kPoolNoSlot && (freem >> lane & 1ull);
+    if (fresh) {  // the new walk: segment, best t, root (traverse_ww's start)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      r.start = mk3(pool.f[0][slot], pool.f[1][slot], pool.f[2][slot]);
+      r.dir = mk3(pool.f[3][slot], pool.f[4][slot], pool.f[5][slot]);
+      h.t = pool.f[6][slot];
+      const uint32_t rw = __float_as_uint(pool.f[7][slot]);
+      zl = (rw & kPoolZl) != 0;
+      w = rw & ~kPoolZl;
+      leaf = 0;
+      sp = 0;
+      h.obj = -1;
+      h.prim = 0;
+      h.u = h.v = 0.0f;
+      h.point = 0;
+      sl = walk_slopes(r, zl);
+      tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+    }
+    if (!__ballot(slot != kPoolNoSlot)) {
+      if (__hip_atomic_load(&pool.alive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    // 3. one pass: inner nodes (while-while, postponed leaves), then the leaves
+    const uint32_t thr = any_pending ? refill : 0u;
+    {
+      const float ix = sl.ix, iy = sl.iy, iz = sl.iz, ox = sl.ox, oy = sl.oy, oz = sl.oz;
+      while (!(w & kLeafBit) && w != kNone) {
+        const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+        float4 X = q[0], Y = q[1], Z = q[2];
+        uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
+        if (COUNT) tally.nodes++;
+        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
+        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
+        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
+        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
+        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
+        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
+        const int tl = __float_as_int(tmax_lim);
+        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
+        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), __int_as_float(min(__float_as_int(fmaxf(g0, k0)), tl)));
+        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
+        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), __int_as_float(min(__float_as_int(fmaxf(g1, k1)), tl)));
+        const bool h0 = n0 <= f0, h1 = n1 <= f1;
+        if (h0 && h1) {
+          const bool swap = n1 < n0;
+          stk[sp * kBlock] = swap ? Cw.x : Cw.y;
+          sp++;
+          w = swap ? Cw.y : Cw.x;
+        } else if (h0 || h1) {
+          w = h0 ? Cw.x : Cw.y;
+        } else {
+          w = sp ? stk[--sp * kBlock] : kNone;
+        }
+        if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
+          leaf = w;
+          w = sp ? stk[--sp * kBlock] : kNone;
+        }
+        if (__ballot(leaf == 0) == 0) break;  // every lane in the loop holds a leaf
+        if ((uint32_t)__popcll(__builtin_amdgcn_read_exec()) <= thr) break;  // few walk: refill first
+      }
+      while (leaf) {  // one triangle per lane per trip (FS_FLAT_LEAF)
+        uint32_t cnt = leaf_count(leaf);
+        if (cnt) {
+          test_leaf<COUNT>(S, leaf_word(1, leaf & kLeafFirstMask), 1, r, zl, h, tally);
+          cnt--;
+        }
+        if (cnt) {
+          leaf = leaf_word(cnt, (leaf & kLeafFirstMask) + 1u);
+        } else if (w & kLeafBit) {
+          leaf = w;
+          w = sp ? stk[--sp * kBlock] : kNone;
+        } else {
+          leaf = 0;
+        }
+      }
+      tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
+    }
+  }
+}
+
 // Conservative segment-vs-box cull for analytic objects (not a reference
 // test): the slab interval uses v_rcp and the same t margins as the BVH
 // traversal, against a box padded on the host (fs_scene.cpp). A segment that
@@ -1188,17 +1379,20 @@ __device__ void scene_trace_tree(const DevScene& S, const Ray& r, MinHit& h, uin
 // SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
 // resume it in a later call with the same ray: objects before the parked one
 // are skipped on resume (already processed), the rest follow in order.
-template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false, bool NOWALK = false>
+template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false, bool NOWALK = false,
+          bool POOL = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
                                                 uint32_t susp_thr_small = 0,
-                                                bool* parked = nullptr) {
+                                                bool* parked = nullptr, WalkPool* pool = nullptr,
+                                                uint32_t sw = 0) {
+  constexpr bool PARK = SUSP || POOL;  // a lane may leave the object loop mid-way and come back
   if (SOCT) {  // Scene::Trace with a valid object tree (scene.cpp:231-236)
     scene_trace_tree<COUNT, TEX>(S, r, h, stk, tally);
     return;
   }
-  bool resuming = SUSP && ws->oi >= 0;
+  bool resuming = PARK && ws->oi >= 0;
   if (!resuming) {
     h.t = 2.0f;
     h.obj = -1;
@@ -1209,6 +1403,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   }
   bool zl = zero_len(r);
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
+  const uint32_t me = sw * kBlock + (threadIdx.x & (kBlock - 1));  // POOL: this lane's slot
   bool park = false;
 #if FS_HOIST_SLOPES
   const Slopes sl = walk_slopes(r, zl);  // once per segment, not once per mesh walk
@@ -1218,7 +1413,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
-    if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
+    if (PARK && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
     int32_t kind = o->kind;
@@ -1226,7 +1421,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     if (kind == FS_OBJ_MESH) {
       if (!o->i2) continue;
       uint64_t t0 = FS_TICK();
-      const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
+      const bool resume_here = PARK && resuming && (uint32_t)ws->oi == oi;
       bool visit = resume_here || ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
       uint64_t t1 = FS_TICK();
       if (o->i3) {  // a small mesh: its faces, no walk (never parks)
@@ -1238,6 +1433,43 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
       } else if (NOWALK) {
         // every mesh of the scene is small (chosen at upload): no BVH walk
+      } else if (POOL) {
+        // the walk goes to the pool: the segment, the best t so far and the
+        // root into this lane's slot; the lane leaves the object loop and
+        // comes back here with the walk's result (kernel: the done bit)
+        const bool submit = visit && !resume_here;
+        if (submit) {
+          pool->f[0][me] = r.start.x;
+          pool->f[1][me] = r.start.y;
+          pool->f[2][me] = r.start.z;
+          pool->f[3][me] = r.dir.x;
+          pool->f[4][me] = r.dir.y;
+          pool->f[5][me] = r.dir.z;
+          pool->f[6][me] = h.t;
+          pool->f[7][me] = __uint_as_float((uint32_t)o->i0 | (zl ? kPoolZl : 0u));
+        }
+        const unsigned long long sm = __ballot(submit);
+        if (sm && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_fetch_or(&pool->pending[sw], sm, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (submit) {
+          ws->oi = (int32_t)oi;
+          park = true;
+          continue;
+        }
+        if (resume_here) {  // the walk of MeshBvhNode::Trace, posted by the walk wave
+          const uint32_t prim = __float_as_uint(pool->f[3][me]);
+          if (prim != kPoolNoSlot) {
+            h.t = pool->f[0][me];
+            h.obj = (int32_t)oi;
+            h.prim = prim;
+            h.u = pool->f[1][me];
+            h.v = pool->f[2][me];
+            h.point = __float_as_uint(pool->f[4][me]);
+          }
+          resuming = false;
+        }
       } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
@@ -1341,7 +1573,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     pa.prim += FS_TICK() - tp0;
 #endif
   }
-  if (SUSP) {
+  if (PARK) {
     if (!park) ws->oi = -1;
     *parked = park;
   }
@@ -1620,8 +1852,8 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 // path, not one block. Each sample's radiance goes to its block's radiance
 // row; fold_groups folds the rows into the frame in sample order.
 template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false,
-          bool NOWALK = false>
-__global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
+          bool NOWALK = false, bool POOL = false>
+__global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                      float2* __restrict__ lvl_all,
                                                                      float4* __restrict__ anchor_all,
                                                                      float4* __restrict__ tex_all,
@@ -1633,20 +1865,47 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   // (c and Ceramic's term, [level][lane]) are staged in LDS instead of HBM
   // scratch rows, so the backward pass reads them at LDS latency and the L2
   // no longer holds (and writes back) the rows.
+  // POOL: the shading waves' rows in LDS too (the walk stack and the pool
+  // take 12 KiB of a 4-wave workgroup's 26 KiB share at 6 waves per SIMD).
+  constexpr bool kLdsRows = NOWALK || (POOL && FS_POOL_LDS_ROWS);
   __shared__ uint32_t stk_all[NOWALK ? 1 : kTraversalStack * kBlock];
-  __shared__ float2 lvl_lds[NOWALK ? kMaxDepth * kBlock : 1];
-  const uint32_t lane = threadIdx.x;
+  __shared__ float2 lvl_lds[kLdsRows ? (POOL ? kPoolWaves - 1 : 1) * kMaxDepth * kBlock : 1];
+  // POOL: workgroups of kPoolWaves waves; wave 0 walks for the others (walk_service)
+  const uint32_t wave = POOL ? threadIdx.x / kBlock : 0u;
+  const uint32_t lane = threadIdx.x % kBlock;
+  const uint32_t wid = POOL ? blockIdx.x * (kPoolWaves - 1) + wave - 1u : blockIdx.x;  // this shading wave's rows
+  WalkPool* pool = nullptr;
+  Tally<COUNT> tally;
+  if constexpr (POOL) {
+    __shared__ WalkPool pool_lds;
+    pool = &pool_lds;
+    if (threadIdx.x < kPoolWaves - 1) {
+      pool->pending[threadIdx.x] = 0;
+      pool->done[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) pool->alive = kPoolWaves - 1;
+    __syncthreads();
+    if (wave == 0) {
+      walk_service<COUNT>(S, *pool, stk_all + lane, P.pool_refill, tally);
+      if (COUNT) {
+        atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
+        atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
+      }
+      return;
+    }
+  }
   uint32_t* stk = stk_all + lane;
   // Scratch rows of the wave, depth-major ([level][lane]) so a wave's store
   // is one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
-  float2* lvl = NOWALK ? lvl_lds : lvl_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);
-  float4* anchor = anchor_all + (size_t)blockIdx.x * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
+  float2* lvl = kLdsRows ? lvl_lds + (POOL ? (wave - 1) * (kMaxDepth * kBlock) : 0u)
+                         : lvl_all + (size_t)wid * (kMaxDepth * kBlock);
+  float4* anchor = anchor_all + (size_t)wid * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
-  float4* texrow = tex_all + (size_t)blockIdx.x * (kMaxDepth * kBlock);  // only touched by textured scenes
+  float4* texrow = tex_all + (size_t)wid * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   TaskBlock cur;  // the block the wave hands out tasks from
   uint32_t queue = blockIdx.x & 7u, queues_left = P.persist ? 8u : 1u;
-  Tally<COUNT> tally;
+  uint32_t idle = 0;  // POOL: iterations in a row in which every lane waited (watchdog)
   uint32_t segments = 0, samples_done = 0;
 
   // the lane's task: its pixel, sample and radiance slot
@@ -1659,7 +1918,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   Ray r;
   uint32_t depth = 0;
   MatTrail<MMAT> mats;
-  mats.row = MMAT ? mat_all + (size_t)blockIdx.x * (kMaxDepth * kBlock) : nullptr;
+  mats.row = MMAT ? mat_all + (size_t)wid * (kMaxDepth * kBlock) : nullptr;
   mats.lane = lane;
   int top = -1;
   bool fresh = true;
@@ -1739,6 +1998,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     FS_PHASE(1);
     const bool aov = (slot >> 31) != 0;
     bool done = false;
+    bool waited = false;  // POOL: the lane only waited for its walk this iteration
     f3 L = mk3(0, 0, 0);
     if (depth >= kMaxDepth) {
       done = true;
@@ -1746,7 +2006,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       L = mk3(1, 1, 1);
       done = true;
     } else {
-      if (!SUSP || ws.oi < 0) segments++;
+      if (!(SUSP || POOL) || ws.oi < 0) segments++;
       bool parked = false;
 #ifdef FS_PHASE_PROF
       PhaseAcc pa;
@@ -1792,11 +2052,58 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       act[1] += (uint64_t)__popcll(__ballot(!(SUSP && parked) && h.obj >= 0));
 #else
       PhaseAcc pa;
-      scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
+      if constexpr (POOL) {
+        // a lane waiting for its walk goes on once the walk wave posted it
+        const unsigned long long dm = lds_load64(&pool->done[wave - 1]);
+        const bool ready = ws.oi >= 0 && ((dm >> lane) & 1ull);
+        parked = ws.oi >= 0 && !ready;
+        // Clear the done bits first: a resumed lane reads its result in the
+        // trace below and may post its next walk into the same slot there,
+        // whose done bit the walk wave can set before this wave goes on.
+        const unsigned long long cm = __ballot(ready);
+        if (cm && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
+          __hip_atomic_fetch_and(&pool->done[wave - 1], ~cm, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!parked)
+          scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK, POOL>(S, r, h, stk, tally, pa, &ws, P.susp_thr,
+                                                                P.susp_thr_small, &parked, pool, wave - 1);
+        if (P.pool_sync) {
+          // Wait (sleeping: the SIMD issues the other waves) for the walks this
+          // wave just posted and finish those lanes' object loops in the same
+          // iteration, so every lane shades its segment together.
+          for (uint32_t round = 0;; round++) {
+            const unsigned long long pm = __ballot(parked);
+            if (!pm) break;
+            uint32_t spins = 0;
+            while ((lds_load64(&pool->done[wave - 1]) & pm) != pm && spins < (1u << 24)) {
+              __builtin_amdgcn_s_sleep(1);
+              spins++;
+            }
+            if (spins >= (1u << 24) || round > 64) {  // a stalled pool: end with a bad frame, not a hang
+              if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) atomicOr(P.status, 1u);
+              if (parked) {
+                ws.oi = -1;
+                h.obj = -1;
+                parked = false;
+              }
+              break;
+            }
+            if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
+              __hip_atomic_fetch_and(&pool->done[wave - 1], ~pm, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (parked) {
+              parked = false;
+              scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK, POOL>(S, r, h, stk, tally, pa, &ws, P.susp_thr,
+                                                                    P.susp_thr_small, &parked, pool, wave - 1);
+            }
+          }
+        }
+        waited = parked;
+      } else {
+        scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
                                                         &parked);
+      }
 #endif
       FS_PHASE(2);
-      if (SUSP && parked) {
+      if ((SUSP || POOL) && parked) {
         // the walk is parked; the lane resumes it next iteration
       } else if (h.obj < 0) {
         if (depth == 1 && (slot & kFog0)) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
@@ -1904,6 +2211,21 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
 #ifdef FS_PHASE_PROF
     ph[8]++;
 #endif
+    if constexpr (POOL) {  // every lane waits: let the walk wave run (and a watchdog for a stalled pool)
+      if (__ballot(!waited)) {
+        idle = 0;
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+        if (++idle > (1u << 24)) {
+          if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) atomicOr(P.status, 1u);
+          break;
+        }
+      }
+    }
+  }
+  if constexpr (POOL) {  // this shading wave is done: the walk wave exits after the last one
+    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
+      __hip_atomic_fetch_sub(&pool->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 #ifdef FS_PHASE_PROF
   ph[9] = __builtin_readcyclecounter() - t_begin;
@@ -2129,6 +2451,7 @@ struct fs_context {
   int nranks = 1, rank = 0;
   DevBuf rows;  // per-lane scratch rows of the lean kernel (LeanRows)
   DevBuf queues;  // per-XCD work-queue counters of the persistent trace kernel
+  DevBuf status;  // kernel status word (Launch::status): bit 0 a walk pool stalled
   uint32_t cus = 0;  // compute units: the persistent grid is one wave per wave slot
 };
 
@@ -2306,6 +2629,12 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 #ifndef FS_NOWALK_WAVES
 #define FS_NOWALK_WAVES 8
 #endif
+// Waves per SIMD of the POOL kernel (workgroups of one walk wave and three
+// shading waves).
+#ifndef FS_POOL_WAVES
+#define FS_POOL_WAVES 6
+#endif
+
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
 
@@ -2318,25 +2647,30 @@ struct LeanKernel {
   LeanFn fn;
   const char* name;
   uint32_t waves;  // waves per SIMD (__launch_bounds__)
+  uint32_t wg;     // waves per workgroup: 1, or kPoolWaves (POOL: a walk wave + shading waves)
 };
-template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false>
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false, bool POOL = false>
 LeanKernel lean_kernel(bool count) {
-  constexpr int W = SUSP ? FS_SUSP_WAVES : NOWALK ? FS_NOWALK_WAVES : FS_LEAN_WAVES;
+  constexpr int W = SUSP ? FS_SUSP_WAVES : NOWALK ? FS_NOWALK_WAVES : POOL ? FS_POOL_WAVES : FS_LEAN_WAVES;
   static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
                                   (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
-                                  (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") +
-                                  (NOWALK ? ", true>" : ", false>");
-  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK>
-                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK>,
-          name.c_str(), (uint32_t)W};
+                                  (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ", " +
+                                  (NOWALK ? "true" : "false") + (POOL ? ", true>" : ", false>");
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK, POOL>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK, POOL>,
+          name.c_str(), (uint32_t)W, POOL ? dev::kPoolWaves : 1u};
 }
 // Scenes traced through the object octree take one instantiation that covers
 // textures and any material count (their object loop is per lane anyway).
 // Untextured scenes whose meshes are all small (no BVH walk) take the NOWALK
 // instantiation: no walk stack, shading rows in LDS.
-LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks) {
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks,
+                       bool pooled) {
   if (object_tree) return lean_kernel<true, false, true, true>(count);
   if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
+  if (pooled)
+    return many_materials ? lean_kernel<false, false, true, false, false, true>(count)
+                          : lean_kernel<false, false, false, false, false, true>(count);
   if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
   if (!walks)
     return many_materials ? lean_kernel<false, false, true, false, true>(count)
@@ -2345,7 +2679,10 @@ LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, b
 }
 
 bool valid_options(const fs_options* o, std::string* why) {
-  if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_PARKED) *why = "unknown schedule";
+  if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_POOL) *why = "unknown schedule";
+  else if (o->schedule == FS_SCHEDULE_POOL && !o->persist) *why = "the POOL schedule needs persist = 1";
+  else if (o->pool_refill > 64) *why = "pool_refill must be 0..64";
+  else if (o->pool_sync > 1) *why = "pool_sync must be 0 or 1";
   else if (o->samples_per_block < 1 || o->samples_per_block > kChunk) *why = "samples_per_block must be 1..64";
   else if (o->xcd_bands > 2) *why = "xcd_bands must be 0, 1 or 2";
   else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..15";
@@ -2396,6 +2733,9 @@ int fs_create(int device, fs_context** out) {
   ctx->cus = cus > 0 ? (uint32_t)cus : 1u;
   FS_HIP(hipMalloc(&ctx->queues.p, 8 * dev::kQueueStride * sizeof(uint32_t)));
   ctx->queues.bytes = 8 * dev::kQueueStride * sizeof(uint32_t);
+  FS_HIP(hipMalloc(&ctx->status.p, 256));
+  ctx->status.bytes = 256;
+  FS_HIP(hipMemset(ctx->status.p, 0, 256));
   *out = ctx.release();
   return FS_OK;
 }
@@ -2407,7 +2747,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
-                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
+                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues, &ctx->status})
     b->release();
   ctx->rows.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -2425,6 +2765,8 @@ int fs_options_default(fs_options* o) {
   o->park_lanes_small = 6;  // C3 (38 k and 209 k-face meshes): 4-6 best
   o->park_min_tris = kParkMinTris;
   o->lds_rows = 1;
+  o->pool_refill = 16;
+  o->pool_sync = 1;
   o->samples_per_block = 16;  // persistent waves: C4 +0.7 %, C3 +2 %, C2 +3 % over 64 (8 and 4 no better)
   o->groups = 0;
   o->group_major = 0;
@@ -2688,6 +3030,9 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // triangles and no texture (the textured instantiation has no parking).
   const bool parked = O.schedule == FS_SCHEDULE_PARKED ||
                       (O.schedule == FS_SCHEDULE_AUTO && ctx->has_parking && !ctx->has_textures && !ctx->scene.tree);
+  const bool pooled = O.schedule == FS_SCHEDULE_POOL;
+  if (pooled && (ctx->has_textures || ctx->scene.tree))
+    return fail(FS_ERR_INVALID, "the POOL schedule does not take textured scenes or object-octree scenes");
   if (parked && ctx->has_textures) return fail(FS_ERR_INVALID, "the PARKED schedule does not take textured scenes");
   if (parked && ctx->scene.tree)
     return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
@@ -2753,15 +3098,20 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   LeanRows rows;
   const bool tree = ctx->scene.tree != nullptr;
   const bool mm = ctx->many_materials || tree;
-  const LeanKernel K =
-      pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr, ctx->has_walks || !O.lds_rows);
+  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked && !pooled, mm, ctx->scene.tree != nullptr,
+                                   ctx->has_walks || !O.lds_rows, pooled);
   // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
-  // K.waves waves per SIMD), never more than the launch has blocks.
+  // K.waves waves per SIMD), never more than the launch has blocks; POOL
+  // workgroups hold K.wg waves, K.wg - 1 of them shading (taking blocks).
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
-  const uint64_t max_grid = O.persist ? std::min<uint64_t>(wave_slots, blocks * G) : blocks * G;
+  const uint64_t shade_per_wg = K.wg > 1 ? K.wg - 1 : 1;
+  auto grid_for = [&](uint64_t nb) {  // workgroups of a launch of nb blocks
+    if (!O.persist) return nb;
+    return std::min<uint64_t>(wave_slots / K.wg, (nb + shade_per_wg - 1) / shade_per_wg);
+  };
   if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
   // On an allocation failure the launches shrink (G halved) until the rows fit.
-  while (blocks && (rc = lean_rows(ctx, std::min<uint64_t>(max_grid, blocks * G) * kBlock, blocks * G * kBlock, chunk,
+  while (blocks && (rc = lean_rows(ctx, grid_for(blocks * G) * shade_per_wg * kBlock, blocks * G * kBlock, chunk,
                                    &rows, ctx->has_textures || tree, mm))) {
     if (G == 1 || O.groups) return rc;
     G = (G + 1) / 2;
@@ -2769,6 +3119,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   }
   ctx->last_kernel = K.name;
   L.persist = O.persist;
+  L.pool_refill = O.pool_refill;
+  L.pool_sync = O.pool_sync;
+  L.status = (uint32_t*)ctx->status.p;
+  FS_HIP(hipMemsetAsync(ctx->status.p, 0, 4, ctx->stream));
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
@@ -2777,9 +3131,9 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     done += L.groups * L.spp;
     ctx->last_launches++;
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
-    const uint32_t grid = (uint32_t)(O.persist ? std::min<uint64_t>(wave_slots, L.nblocks) : L.nblocks);
+    const uint32_t grid = (uint32_t)grid_for(L.nblocks);
     if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
-    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
+    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock * K.wg), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
                        rows.tex, rows.rad, rows.mat, (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
     hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
     FS_HIP(hipGetLastError());
@@ -2788,12 +3142,21 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   return FS_OK;
 }
 
+// The kernels' status word after the stream has drained (a stalled walk
+// pool's watchdog ends the kernel with a bad frame instead of hanging).
+int check_status(fs_context* ctx) {
+  uint32_t st = 0;
+  FS_HIP(hipMemcpy(&st, ctx->status.p, 4, hipMemcpyDeviceToHost));
+  if (st & 1u) return fail(FS_ERR_DEVICE, "walk pool stalled (watchdog): the frame is invalid");
+  return FS_OK;
+}
+
 int fs_synchronize(fs_context* ctx) {
   if (!ctx) return fail(FS_ERR_INVALID, "null context");
   int rc;
   if ((rc = set_device(ctx))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
-  return FS_OK;
+  return check_status(ctx);
 }
 
 const char* fs_last_kernel(fs_context* ctx) { return ctx ? ctx->last_kernel : ""; }
@@ -2811,7 +3174,7 @@ int fs_last_render_ms(fs_context* ctx, float* ms) {
   if ((rc = set_device(ctx))) return rc;
   FS_HIP(hipEventSynchronize(ctx->ev1));
   FS_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
-  return FS_OK;
+  return check_status(ctx);
 }
 
 int fs_read_counters(fs_context* ctx, fs_counters* out) {
@@ -2903,6 +3266,110 @@ int fs_prepare_digest(const fs_scene_desc* desc, const fs_options* opt, uint64_t
   *digest = h;
   if (num_nodes) *num_nodes = P.nodes.size();
   if (build_ms) *build_ms = P.build_ms;
+  return FS_OK;
+}
+
+// Tree quality of every BVH mesh of a host-side preparation (measurement aid,
+// no reference counterpart): per mesh the SAH cost relative to its root box
+// (inner nodes 1, triangle tests 1 per face: sum over nodes of area/root
+// area), the overlap of sibling boxes (area of child0 ∩ child1 over the
+// parent's area, mean per depth level and area-weighted total), node, leaf
+// and face counts and the depth. Written as JSON into out (size bytes).
+int fs_bvh_quality(const fs_scene_desc* desc, const fs_options* opt, char* out, size_t size) {
+  if (!desc || !out || !size) return fail(FS_ERR_INVALID, "null argument");
+  std::string err;
+  if (opt && !valid_options(opt, &err)) return fail(FS_ERR_INVALID, "fs_bvh_quality: " + err);
+  PreparedScene P;
+  int rc = prepare_scene(desc, &P, &err, BuildOptions::from(opt));
+  if (rc) return fail(rc, err);
+  struct B3 {
+    float lo[3], hi[3];
+  };
+  auto area = [](const B3& b) {
+    float d[3];
+    for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, b.hi[k] - b.lo[k]);
+    return 2.0 * ((double)d[0] * d[1] + (double)d[1] * d[2] + (double)d[2] * d[0]);
+  };
+  auto child_box = [&](const BvhNode& n, int c) {
+    B3 b;
+    b.lo[0] = n.lo_x[c]; b.hi[0] = n.hi_x[c];
+    b.lo[1] = n.lo_y[c]; b.hi[1] = n.hi_y[c];
+    b.lo[2] = n.lo_z[c]; b.hi[2] = n.hi_z[c];
+    return b;
+  };
+  std::string js = "[";
+  for (size_t oi = 0; oi < P.objects.size(); oi++) {
+    const DevObject& o = P.objects[oi];
+    if (o.kind != FS_OBJ_MESH || !o.i2 || o.i3) continue;  // BVH meshes only
+    struct Item {
+      uint32_t node, depth;
+      B3 box;
+    };
+    const BvhNode& rn = P.nodes[(uint32_t)o.i0];
+    B3 root;
+    for (int k = 0; k < 3; k++) {
+      B3 a = child_box(rn, 0), b = child_box(rn, 1);
+      root.lo[k] = std::min(a.lo[k], b.lo[k]);
+      root.hi[k] = std::max(a.hi[k], b.hi[k]);
+    }
+    const double ar = std::max(area(root), 1e-30);
+    double sah = 0.0, ov_w = 0.0;
+    uint64_t nodes = 0, leaves = 0, faces = 0;
+    uint32_t depth = 0;
+    std::vector<double> ov_sum, ov_n;
+    std::vector<Item> st{{(uint32_t)o.i0, 0, root}};
+    while (!st.empty()) {
+      Item it = st.back();
+      st.pop_back();
+      const BvhNode& n = P.nodes[it.node];
+      nodes++;
+      depth = std::max(depth, it.depth);
+      const double a = area(it.box);
+      sah += a / ar;
+      B3 c0 = child_box(n, 0), c1 = child_box(n, 1), x;
+      for (int k = 0; k < 3; k++) {
+        x.lo[k] = std::max(c0.lo[k], c1.lo[k]);
+        x.hi[k] = std::min(c0.hi[k], c1.hi[k]);
+      }
+      bool disjoint = false;
+      for (int k = 0; k < 3; k++) disjoint |= x.lo[k] > x.hi[k];
+      const double ov = disjoint || a <= 0 ? 0.0 : area(x) / a;
+      if (ov_sum.size() <= it.depth) {
+        ov_sum.resize(it.depth + 1, 0.0);
+        ov_n.resize(it.depth + 1, 0.0);
+      }
+      ov_sum[it.depth] += ov;
+      ov_n[it.depth] += 1.0;
+      ov_w += ov * a / ar;
+      for (int c = 0; c < 2; c++) {
+        const uint32_t w = n.child[c];
+        const B3 cb = child_box(n, c);
+        if (w & kLeafBit) {
+          leaves++;
+          faces += leaf_count(w);
+          sah += area(cb) / ar * leaf_count(w);
+          depth = std::max(depth, it.depth + 1);
+        } else {
+          st.push_back({w, it.depth + 1, cb});
+        }
+      }
+    }
+    char buf[256];
+    std::snprintf(buf, sizeof buf,
+                  "%s{\"object\": %zu, \"nodes\": %llu, \"leaves\": %llu, \"faces\": %llu, \"depth\": %u, "
+                  "\"sah_cost\": %.4f, \"overlap_weighted\": %.4f, \"overlap_per_level\": [",
+                  js.size() > 1 ? ", " : "", oi, (unsigned long long)nodes, (unsigned long long)leaves,
+                  (unsigned long long)faces, depth, sah, ov_w);
+    js += buf;
+    for (size_t l = 0; l < ov_sum.size(); l++) {
+      std::snprintf(buf, sizeof buf, "%s%.4f", l ? ", " : "", ov_n[l] ? ov_sum[l] / ov_n[l] : 0.0);
+      js += buf;
+    }
+    js += "]}";
+  }
+  js += "]";
+  if (js.size() + 1 > size) return fail(FS_ERR_INVALID, "fs_bvh_quality: output buffer too small");
+  std::memcpy(out, js.c_str(), js.size() + 1);
   return FS_OK;
 }
 

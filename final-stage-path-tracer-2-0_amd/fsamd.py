@@ -99,11 +99,12 @@ class fs_options(C.Structure):
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
                 ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
                 ("park_entry", C.c_uint32), ("park_entry_small", C.c_uint32),
-                ("lds_rows", C.c_uint32)]
+                ("lds_rows", C.c_uint32), ("pool_refill", C.c_uint32),
+                ("pool_sync", C.c_uint32)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
-SCHEDULES = {"auto": 0, "lean": 1, "parked": 2}  # fs_schedule
+SCHEDULES = {"auto": 0, "lean": 1, "parked": 2, "pool": 3}  # fs_schedule
 NODE_LAYOUTS = {"depth_first": 0, "pairs": 1}
 
 # Exported symbols of include/fs_trace.h, with their ctypes signatures.
@@ -136,6 +137,7 @@ GPU_SYMBOLS = {
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
     "fs_comm_count": ([_VP, C.POINTER(C.c_int)], C.c_int),
+    "fs_bvh_quality": ([_VP, C.POINTER(fs_options), C.c_char_p, C.c_size_t], C.c_int),
     "fs_comm_destroy": ([_VP], C.c_int),
     "fs_frame_pack_bytes": ([C.POINTER(fs_render_params), C.POINTER(C.c_uint64)], C.c_int),
     "fs_frame_pack": ([_VP, _VP, C.POINTER(fs_render_params), _VP, C.c_size_t], C.c_int),
@@ -550,6 +552,16 @@ def load_exr(path):
         return np.ctypeslib.as_array(buf, shape=(h.value * w.value * 4,)).reshape(h.value, w.value, 4).copy()
     finally:
         lib.fsh_free(buf)
+
+
+def bvh_quality(desc_ptr, **opts):
+    """fs_bvh_quality: per BVH mesh SAH cost, sibling overlap, counts, depth."""
+    import json
+
+    buf = C.create_string_buffer(1 << 20)
+    o = options(**opts)
+    _check(gpu_lib().fs_bvh_quality(desc_ptr, C.byref(o), buf, len(buf)), "fs_bvh_quality")
+    return json.loads(buf.value.decode())
 
 
 def prepare_digest(desc_ptr, **opts):

@@ -230,7 +230,9 @@ typedef enum fs_schedule {
   FS_SCHEDULE_AUTO = 0,   /* PARKED when the scene has a mesh of >= park_min_tris
                              triangles and no texture, else LEAN */
   FS_SCHEDULE_LEAN = 1,   /* path-regeneration megakernel, pooled (pixel, sample) tasks */
-  FS_SCHEDULE_PARKED = 2  /* LEAN + BVH walks of large meshes park when few lanes walk */
+  FS_SCHEDULE_PARKED = 2, /* LEAN + BVH walks of large meshes park when few lanes walk */
+  FS_SCHEDULE_POOL = 3    /* workgroups of 4 waves: one walks every BVH for the other three
+                             (an LDS pool of segments), which shade; needs persist = 1 */
 } fs_schedule;
 
 #define FS_NODE_LAYOUT_DEPTH_FIRST 0u
@@ -270,6 +272,11 @@ typedef struct fs_options {
   uint32_t park_entry_small;   /* the same for the smaller parkable meshes (0 = off; 0..64) */
   uint32_t lds_rows;           /* 1: scenes without BVH walks (every mesh small, no texture) run
                                   the NOWALK kernel, shading rows in LDS (1); 0 the LEAN kernel */
+  uint32_t pool_refill;        /* POOL: the walk wave takes pending walks once at most this many
+                                  of its lanes still walk (16; 0..64) */
+  uint32_t pool_sync;          /* POOL: 1 a shading wave sleeps until the walks it posted are done
+                                  and finishes those segments in the same iteration (1); 0 the
+                                  lanes wait for the next iteration */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */
@@ -353,6 +360,13 @@ int fs_frame_pack_bytes(const fs_render_params* params, uint64_t* bytes);
 int fs_frame_pack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, void* host_dst, size_t bytes);
 int fs_frame_unpack(fs_context* ctx, fs_frame* frame, const fs_render_params* params, const void* host_src,
                     size_t bytes);
+
+/* Tree quality of every BVH mesh of a host-side preparation with the build
+ * fields of opt (NULL: defaults), as JSON: per mesh the SAH cost relative to
+ * its root box, the sibling-box overlap per depth level and area-weighted,
+ * node / leaf / face counts and depth. Measurement aid, no device needed,
+ * no reference counterpart. */
+int fs_bvh_quality(const fs_scene_desc* desc, const fs_options* opt, char* out, size_t size);
 
 /* Host only (no device needed): runs the scene preparation of
  * fs_upload_scene (object constructors, host BVH build, with the build

@@ -36,13 +36,13 @@ def code_object(so_path, target="gfx950"):
 
 
 def demangle_lean(name):
-    """render_kernel_lean<b, W, b, b, b, b, b> as fs_last_kernel names it."""
-    m = re.search(r"render_kernel_leanIL(b[01])ELi(\d+)EL(b[01])EL(b[01])EL(b[01])EL(b[01])EL(b[01])E", name)
+    """render_kernel_lean<b, W, b, ...> as fs_last_kernel names it."""
+    m = re.search(r"render_kernel_leanIL(b[01])ELi(\d+)E((?:L(?:b[01])E)+)", name)
     if not m:
         return None
     b = lambda t: "true" if t == "b1" else "false"  # noqa: E731
-    return (f"render_kernel_lean<{b(m.group(1))}, {m.group(2)}, {b(m.group(3))}, {b(m.group(4))}, "
-            f"{b(m.group(5))}, {b(m.group(6))}, {b(m.group(7))}>")
+    rest = [b(t) for t in re.findall(r"L(b[01])E", m.group(3))]
+    return f"render_kernel_lean<{b(m.group(1))}, {m.group(2)}, " + ", ".join(rest) + ">"
 
 
 def kernel_resources(so_path=None):

@@ -15,6 +15,16 @@ import sys
 from collections import defaultdict
 
 
+def kernel_durations(pmc_dir, kname):
+    """Mean duration (s) of the kernel's dispatches in the passes' kernel traces."""
+    d = []
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "*", "*kernel_trace.csv"))):
+        for row in csv.DictReader(open(f)):
+            if kname in row["Kernel_Name"]:
+                d.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    return sum(d) / len(d) if d else None
+
+
 def main():
     pmc_dir, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
     note = sys.argv[4] if len(sys.argv) > 4 else ""
@@ -51,6 +61,28 @@ def main():
         res["wait_any_frac"] = round(avg["SQ_WAIT_ANY"] / max(avg["SQ_WAVE_CYCLES"], 1), 4)
     if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
         res["valu_lane_util"] = round(avg["SQ_THREAD_CYCLES_VALU"] / max(64 * avg["SQ_ACTIVE_INST_VALU"], 1), 4)
+    if samples and "SQ_INSTS_VALU" in avg:
+        res["valu_insts_per_sample"] = round(avg["SQ_INSTS_VALU"] / samples, 3)
+        if "SQ_INSTS_SALU" in avg:
+            res["salu_insts_per_sample"] = round(avg["SQ_INSTS_SALU"] / samples, 3)
+    if samples and "SQ_ACTIVE_INST_VALU" in avg:
+        # quad-cycles (4 SIMD cycles) of VALU issue per sample, summed over waves
+        res["valu_active_quads_per_sample"] = round(avg["SQ_ACTIVE_INST_VALU"] / samples, 3)
+    dur = kernel_durations(pmc_dir, kname)
+    if dur:
+        res["kernel_ms"] = round(dur * 1e3, 3)
+    if "GRBM_GUI_ACTIVE" in avg and dur:
+        # MI355X_MICROARCH.md (DVFS): effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+        clock = avg["GRBM_GUI_ACTIVE"] / 8 / dur
+        res["clock_ghz"] = round(clock / 1e9, 3)
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            # VALUBusy (rocprof's gfx9 formula): VALU issue quad-cycles x 4 over the 1024 SIMDs' cycles.
+            # On gfx950 it can exceed 1: two waves' wave64 FP32 instructions share a 4-cycle window
+            res["valu_busy"] = round(avg["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8), 4)
+        if "SQ_INSTS_VALU" in avg:
+            # VALU issue against its peak: a wave64 FP32 instruction every 2 cycles per SIMD
+            # (MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc; = 157.3 TF FP32 at full lanes)
+            res["valu_issue_frac"] = round(avg["SQ_INSTS_VALU"] * 2 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8), 4)
     res["method"] = ("rocprofv3 --pmc, one counter group per pass (tools/gpu_pmc.sh); FETCH_SIZE KiB x1024 x2 "
                      "(gfx950 half-count, MI355X_MICROARCH.md §HBM) + WRITE_SIZE KiB x1024; per dispatch average")
     if note:
