@@ -58,6 +58,11 @@
 #ifndef FS_POOL_LDS_ROWS
 #define FS_POOL_LDS_ROWS 1
 #endif
+// Object loop: each record's first 64 B as one scalar load (1) or each field
+// where it is first used (0, A/B)
+#ifndef FS_OBJ_HEAD
+#define FS_OBJ_HEAD 1
+#endif
 #ifndef FS_RAD_XYZ
 #define FS_RAD_XYZ 1
 #endif
@@ -709,6 +714,35 @@ __device__ __forceinline__ uint8_t gamma8(float c) {  // frame.cpp:67-71
 typedef const __attribute__((address_space(4))) DevObject* ConstObj;
 __device__ __forceinline__ ConstObj const_obj(const DevObject* base, uint32_t i) {
   return (ConstObj)(base) + i;
+}
+
+// The first 64 B of an object record (kind, material, i0-i5, d0-d7): what the
+// object loop reads for meshes, spheres, planes and discs, fetched as one
+// scalar load at the top of the object's iteration (FS_OBJ_HEAD) instead of
+// field by field where each is first used (three or four dependent scalar
+// round trips per object).
+struct ObjHead {
+  int32_t kind, mat, i0, i1, i2, i3, i4, i5;
+  float d[8];
+};
+typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+__device__ __forceinline__ ObjHead load_head(ConstObj o) {
+  ConstU32 q = (ConstU32)o;
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = q[i];  // adjacent: one s_load_dwordx16
+  ObjHead H;
+  H.kind = (int32_t)w[0];
+  H.mat = (int32_t)w[1];
+  H.i0 = (int32_t)w[2];
+  H.i1 = (int32_t)w[3];
+  H.i2 = (int32_t)w[4];
+  H.i3 = (int32_t)w[5];
+  H.i4 = (int32_t)w[6];
+  H.i5 = (int32_t)w[7];
+#pragma unroll
+  for (int i = 0; i < 8; i++) H.d[i] = __uint_as_float(w[8 + i]);
+  return H;
 }
 
 struct MinHit {
@@ -1416,17 +1450,24 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     if (PARK && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
-    int32_t kind = o->kind;
+#if FS_OBJ_HEAD
+    const ObjHead H = load_head(o);
+    const float* hd = H.d;
+#else
+    const auto& H = *o;
+    const __attribute__((address_space(4))) float* hd = o->d;
+#endif
+    const int32_t kind = H.kind;
     const __attribute__((address_space(4))) float* d = o->d;
     if (kind == FS_OBJ_MESH) {
-      if (!o->i2) continue;
+      if (!H.i2) continue;
       uint64_t t0 = FS_TICK();
       const bool resume_here = PARK && resuming && (uint32_t)ws->oi == oi;
-      bool visit = resume_here || ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t);
+      bool visit = resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t);
       uint64_t t1 = FS_TICK();
-      if (o->i3) {  // a small mesh: its faces, no walk (never parks)
+      if (H.i3) {  // a small mesh: its faces, no walk (never parks)
         if (visit)
-          small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
+          small_mesh_trace<COUNT>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
 #ifdef FS_PHASE_PROF
         pa.small += FS_TICK() - t1;
         t1 = FS_TICK();
@@ -1446,7 +1487,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
           pool->f[4][me] = r.dir.y;
           pool->f[5][me] = r.dir.z;
           pool->f[6][me] = h.t;
-          pool->f[7][me] = __uint_as_float((uint32_t)o->i0 | (zl ? kPoolZl : 0u));
+          pool->f[7][me] = __uint_as_float((uint32_t)H.i0 | (zl ? kPoolZl : 0u));
         }
         const unsigned long long sm = __ballot(submit);
         if (sm && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) {
@@ -1476,12 +1517,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         // thresholds: bits 0-7 park a walk when at most this many lanes still
         // walk; bits 8-15 defer the walk's start (park at the root) while
         // fewer lanes than this want to walk and other lanes can go on
-        const uint32_t thr = o->i5 == 2 ? susp_thr : (o->i5 ? susp_thr_small : 0u);
+        const uint32_t thr = H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u);
         if (thr >> 8) {
           const uint32_t want = (uint32_t)__popcll(__ballot(visit));
           if (visit && !resume_here && want < (thr >> 8) && want < (uint32_t)__builtin_amdgcn_readfirstlane(live)) {
             ws->oi = (int32_t)oi;  // parked at the root: the walk starts from there on resume
-            ws->w = (uint32_t)o->i0;
+            ws->w = (uint32_t)H.i0;
             ws->leaf = 0;
             ws->sp = 0;
             park = true;
@@ -1489,7 +1530,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
           }
         }
         if (visit)
-          park = traverse_ww<COUNT, true>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
+          park = traverse_ww<COUNT, true>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
                                           thr & 0xFFu, live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
@@ -1500,11 +1541,11 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
         if (park) continue;
       } else if (visit) {
-        traverse_ww<COUNT>(S, (uint32_t)o->i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+        traverse_ww<COUNT>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
       }
       // MeshObject::Trace writes surface_texcoords only when the mesh has
       // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
-      if (TEX && h.obj == (int32_t)oi && o->i4) h.tc = (int32_t)oi;
+      if (TEX && h.obj == (int32_t)oi && H.i4) h.tc = (int32_t)oi;
 #ifdef FS_PHASE_PROF
       uint64_t t2 = FS_TICK();
       pa.cull += t1 - t0;
@@ -1523,18 +1564,18 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     float t;
     f3 p, n;
     if (kind == FS_OBJ_SPHERE) {
-      if (ray_sphere(mk3(d[0], d[1], d[2]), d[3], r, t, p, n) && t < h.t) {
+      if (ray_sphere(mk3(hd[0], hd[1], hd[2]), hd[3], r, t, p, n) && t < h.t) {
         h.t = t;
         h.obj = (int32_t)oi;
       }
     } else if (kind == FS_OBJ_PLANE) {
-      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p) && t < h.t) {
+      if (ray_plane(mk4(hd[0], hd[1], hd[2], hd[3]), r, t, p) && t < h.t) {
         h.t = t;
         h.obj = (int32_t)oi;
       }
     } else if (kind == FS_OBJ_DISC) {
-      if (ray_plane(mk4(d[0], d[1], d[2], d[3]), r, t, p)) {
-        if (length(mk3(d[4], d[5], d[6]) - p) <= d[7] && t < h.t) {
+      if (ray_plane(mk4(hd[0], hd[1], hd[2], hd[3]), r, t, p)) {
+        if (length(mk3(hd[4], hd[5], hd[6]) - p) <= hd[7] && t < h.t) {
           h.t = t;
           h.obj = (int32_t)oi;
         }

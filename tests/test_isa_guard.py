@@ -23,7 +23,7 @@ LIMITS = {
     "render_kernel_lean<false, 6, false, false, false, false, false, false>": (16, 10, 80),
     # LEAN without walks (NOWALK: every mesh small, shading rows in LDS, 8 waves
     # per SIMD): C1 and C2
-    "render_kernel_lean<false, 8, false, false, false, false, true, false>": (32, 24, 64),
+    "render_kernel_lean<false, 8, false, false, false, false, true, false>": (32, 27, 64),
 }
 
 
