@@ -20,7 +20,7 @@ LIMITS = {
     # PARKED schedule: C3 and C4 (the bench kernel)
     "render_kernel_lean<false, 6, false, true, false, false, false, false>": (44, 21, 80),
     # LEAN schedule: scenes with BVH walks and no large mesh
-    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (16, 10, 80),
+    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (16, 12, 80),
     # LEAN without walks (NOWALK: every mesh small, shading rows in LDS, 8 waves
     # per SIMD): C1 and C2
     "render_kernel_lean<false, 8, false, false, false, false, true, false>": (32, 27, 64),
