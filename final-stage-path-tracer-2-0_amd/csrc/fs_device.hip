@@ -1514,24 +1514,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
-        // thresholds: bits 0-7 park a walk when at most this many lanes still
-        // walk; bits 8-15 defer the walk's start (park at the root) while
-        // fewer lanes than this want to walk and other lanes can go on
-        const uint32_t thr = H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u);
-        if (thr >> 8) {
-          const uint32_t want = (uint32_t)__popcll(__ballot(visit));
-          if (visit && !resume_here && want < (thr >> 8) && want < (uint32_t)__builtin_amdgcn_readfirstlane(live)) {
-            ws->oi = (int32_t)oi;  // parked at the root: the walk starts from there on resume
-            ws->w = (uint32_t)H.i0;
-            ws->leaf = 0;
-            ws->sp = 0;
-            park = true;
-            continue;
-          }
-        }
+        // (deferring a walk's start until enough lanes want it, parked at the
+        // root: C4 -1 to -10 %, C3 -11 to +1.6 %, and its code alone cost C3
+        // 1.3 %: removed)
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
-                                          thr & 0xFFu, live, slp);
+                                          H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u), live, slp);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
         if (park) {
@@ -2732,7 +2720,6 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->persist > 1) *why = "persist must be 0 or 1";
   else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
   else if (o->park_lanes > 64 || o->park_lanes_small > 64) *why = "park_lanes must be 0..64";
-  else if (o->park_entry > 64 || o->park_entry_small > 64) *why = "park_entry must be 0..64";
   else if (o->lds_rows > 1) *why = "lds_rows must be 0 or 1";
   else return true;
   return false;
@@ -3048,8 +3035,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   L.tile_stride = stride;
   L.seed = params->seed;
   const fs_options& O = ctx->opt;
-  L.susp_thr = O.park_lanes | (O.park_entry << 8);
-  L.susp_thr_small = O.park_lanes_small | (O.park_entry_small << 8);
+  L.susp_thr = O.park_lanes;
+  L.susp_thr_small = O.park_lanes_small;
   // XCD placement: 0 dispatch order, 1 one band per XCD (C4 -25 %: the bands
   // are unbalanced), 2 (default) whole 64x64 tiles per XCD (C4 +1.5 %)
   L.xcd_bands = O.xcd_bands;

@@ -98,7 +98,6 @@ class fs_options(C.Structure):
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
                 ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
-                ("park_entry", C.c_uint32), ("park_entry_small", C.c_uint32),
                 ("lds_rows", C.c_uint32), ("pool_refill", C.c_uint32),
                 ("pool_sync", C.c_uint32)]
 
@@ -175,9 +174,20 @@ _gpu = None
 _host = None
 
 
+# Entry points added after ABI 4. A measurement build of an earlier round
+# (tools/lib_ab.sh A/B against an older libfsgpu.so, selected by
+# FSAMD_GPU_LIB) may lack them; the product library always has them.
+_OPTIONAL = {"fs_comm_count", "fs_bvh_quality"}
+
+
 def _bind(lib, table):
     for name, (args, res) in table.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if name in _OPTIONAL and os.environ.get("FSAMD_GPU_LIB"):
+                continue
+            raise
         fn.argtypes = args
         fn.restype = res
     return lib

@@ -266,10 +266,6 @@ typedef struct fs_options {
                                   face by face with wave-uniform loads, no BVH walk (16; 0 off,
                                   max 64); read at upload */
   uint32_t park_lanes_small;   /* PARKED: park_lanes for parkable meshes under 2^19 triangles (6) */
-  uint32_t park_entry;         /* PARKED: a walk of a mesh of >= 2^19 triangles starts only when at
-                                  least this many lanes want it (or no other lane can go on);
-                                  the others wait parked at the root (0 = off; 0..64) */
-  uint32_t park_entry_small;   /* the same for the smaller parkable meshes (0 = off; 0..64) */
   uint32_t lds_rows;           /* 1: scenes without BVH walks (every mesh small, no texture) run
                                   the NOWALK kernel, shading rows in LDS (1); 0 the LEAN kernel */
   uint32_t pool_refill;        /* POOL: the walk wave takes pending walks once at most this many

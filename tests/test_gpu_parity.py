@@ -563,7 +563,6 @@ OPTION_VARIANTS = [
     {"schedule": "parked", "park_min_tris": 1},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63, "park_lanes_small": 63},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes_small": 1},
-    {"schedule": "parked", "park_min_tris": 1, "park_entry": 48, "park_entry_small": 64},
     {"schedule": "pool"},
     {"schedule": "pool", "pool_refill": 0, "pool_sync": 0},
     {"schedule": "pool", "pool_refill": 64, "small_mesh_tris": 0},
