@@ -206,6 +206,9 @@ __device__ __forceinline__ bool ref_bounds_hit(f3 mn, f3 mx, const Ray& r, bool 
 // is close too (FS_ROOT_PAIRS). A flat box (a wall, a quad light: n_i = f_i)
 // no longer takes the exact path wherever it is hit: C2 +5.7 %, C4 +3.4 %.
 __device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best) {
+#ifdef FS_MEAS_ROOT_ALL  // measurement builds only: every mesh root visited (frames differ)
+  return !zl || in_bounds(mn, mx, r.start);
+#endif
   bool si = in_bounds(mn, mx, r.start);
   if (zl) return si;                                 // param 0 (intersect.cpp:604-616)
   if (si && in_bounds(mn, mx, r.stop)) return true;  // param 0 (:621-630)
@@ -2219,7 +2222,11 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
         p0 = mk3(a.x, a.y, a.z);
         lp0 = mk3(b.x, b.y, b.z);
       }
+#ifndef FS_MEAS_NO_UNWIND  // measurement builds only: no backward pass (frames differ)
       L = unwind<TEX, MMAT, !SUSP>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
+#else
+      L.x += (float)top + p0.x + lp0.x;
+#endif
       float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);
       const uint32_t o = slot & ~(0x80000000u | kFog0);
 #ifndef FS_MEAS_NO_RAD

@@ -50,8 +50,10 @@ class FileGroup:
     for a rank when the files it waits for exist. The files of operation k
     are deleted once operation k + 1 has completed (every rank has then left
     k); close() ends with a "done" file per rank, after which rank 0 removes
-    the directory. abort() (a rank that fails) removes the rank's own files,
-    and rank 0's removes the directory.
+    the directory. abort() (a rank that fails) leaves an "abort" file and
+    removes the rank's own files, and rank 0's removes the directory; a rank
+    waiting in any operation sees either and raises at once, instead of
+    waiting out its timeout.
     """
 
     def __init__(self, rank: int, world: int, path: str | None = None, timeout: float = 900.0,
@@ -88,10 +90,21 @@ class FileGroup:
                     still.append(r)
             pending = still
             if pending:
+                self._check_abort()
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"rendezvous {self.path}: op {seq} still waits for ranks {pending}")
                 time.sleep(self.poll)
         return out
+
+    def _check_abort(self) -> None:
+        marker = os.path.join(self.path, "abort")
+        if os.path.exists(marker) or not os.path.isdir(self.path):
+            try:
+                with open(marker) as f:
+                    who = f.read().strip()
+            except OSError:
+                who = "0"
+            raise RuntimeError(f"rendezvous {self.path}: rank {who} aborted")
 
     def _done(self, seq: int) -> None:
         # every rank has completed seq, hence left seq - 1: drop our file of it
@@ -142,8 +155,15 @@ class FileGroup:
         return [list(struct.unpack(f"<{len(got[r]) // 8}d", got[r])) for r in range(self.world)]
 
     def abort(self) -> None:
-        """Clean-up of a rank that fails: its own files go; rank 0 removes the
-        directory (other ranks then time out instead of reading stale files)."""
+        """Clean-up of a rank that fails: an "abort" marker for the others,
+        then its own files go; rank 0 removes the directory."""
+        try:
+            tmp = os.path.join(self.path, f"abort.{self.rank}.tmp")
+            with open(tmp, "w") as f:
+                f.write(str(self.rank))
+            os.replace(tmp, os.path.join(self.path, "abort"))
+        except OSError:
+            pass
         try:
             for name in os.listdir(self.path):
                 if name.split(".")[1:2] == [str(self.rank)]:

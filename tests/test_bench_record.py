@@ -96,3 +96,33 @@ def test_rendezvous_abort_removes_stale_files(tmp_path):
     assert not os.path.exists(path)
     # the default directory carries the launcher's start time as a nonce
     assert rendezvous._start_time(os.getppid()) != "0"
+
+
+def test_rendezvous_abort_wakes_waiting_ranks(tmp_path):
+    """A rank blocked in a collective raises as soon as another rank aborts,
+    long before its own timeout."""
+    import threading
+    import time
+
+    import rendezvous
+
+    path = str(tmp_path / "g")
+    waiting = rendezvous.FileGroup(1, 2, path=path, timeout=60.0)
+    failing = rendezvous.FileGroup(0, 2, path=path, timeout=60.0)
+    seen = {}
+
+    def wait():
+        t0 = time.monotonic()
+        try:
+            waiting.barrier()
+        except RuntimeError as e:
+            seen["err"] = str(e)
+        seen["s"] = time.monotonic() - t0
+
+    th = threading.Thread(target=wait)
+    th.start()
+    time.sleep(0.2)
+    failing.abort()
+    th.join(10)
+    assert not th.is_alive()
+    assert "rank 0 aborted" in seen["err"] and seen["s"] < 5
