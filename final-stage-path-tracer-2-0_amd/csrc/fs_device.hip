@@ -60,6 +60,18 @@
 #endif
 // Object loop: each record's first 64 B as one scalar load (1) or each field
 // where it is first used (0, A/B)
+#ifndef FS_ROOT_BF  // mesh-root cull as straight-line masks (1) or early returns (0)
+#define FS_ROOT_BF 1
+#endif
+#ifndef FS_ROOT_TOL  // FS_ROOT_BF: margins of the fast cull from its error bound (1) or 1e-5 (0)
+#define FS_ROOT_TOL 1
+#endif
+#ifndef FS_ROOT_LITE  // FS_ROOT_BF: the exact path as straight-line code (1) or ref_ray_bounds (0)
+#define FS_ROOT_LITE 1
+#endif
+#ifndef FS_ROOT_HOIST  // FS_ROOT_BF: the segment's slopes computed once for every mesh root (1)
+#define FS_ROOT_HOIST 1
+#endif
 #ifndef FS_OBJ_HEAD
 #define FS_OBJ_HEAD 1
 #endif
@@ -192,6 +204,56 @@ __device__ __forceinline__ bool ref_bounds_hit(f3 mn, f3 mx, const Ray& r, bool 
   return true;
 }
 
+// Per-ray slab constants of the BVH walks, computed once per segment. A
+// zero-length ray (a point test at the leaves) walks with a 1e-20 slope per
+// axis: every box that contains the start passes the slab test (entry <= 0 <=
+// exit), so the cull stays a superset of the point-in-box test without a
+// per-node branch. v_rcp (about 1 ulp) instead of IEEE division: the slab
+// test is a conservative cull whose t margins (1e-6 absolute, 2e-6 relative)
+// and box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
+struct Slopes {
+  float ix, iy, iz, ox, oy, oz;
+};
+__device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl, f3 dir) {
+  const float tiny = 1e-20f;
+  float dx = fabsf(dir.x) < tiny || zl ? copysignf(tiny, dir.x) : dir.x;
+  float dy = fabsf(dir.y) < tiny || zl ? copysignf(tiny, dir.y) : dir.y;
+  float dz = fabsf(dir.z) < tiny || zl ? copysignf(tiny, dir.z) : dir.z;
+  Slopes sl;
+  sl.ix = __builtin_amdgcn_rcpf(dx);
+  sl.iy = __builtin_amdgcn_rcpf(dy);
+  sl.iz = __builtin_amdgcn_rcpf(dz);
+  sl.ox = -r.start.x * sl.ix;
+  sl.oy = -r.start.y * sl.iy;
+  sl.oz = -r.start.z * sl.iz;
+  return sl;
+}
+__device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) { return walk_slopes(r, zl, r.dir); }
+// The object loop's slopes (FS_ROOT_HOIST): from the segment stop - start, the
+// v of the reference's ray_intersect_bounds (intersect.cpp:531-597), so the
+// mesh-root culls reuse them (the reversed segment's slopes are their
+// negation, exactly); the walks cull with them as well (dir and stop - start
+// differ by rounding only, far inside the walk's margins).
+__device__ __forceinline__ Slopes seg_slopes(const Ray& r, bool zl) { return walk_slopes(r, zl, r.stop - r.start); }
+
+
+#ifdef FS_PHASE_PROF
+// Mesh-root cull outcomes (profiling build): lanes tested, lanes sent to the
+// reference's divisions, and why (parallel slab, fnear~ffar with a close
+// cross-slab pair, fnear~1, param~best). Wave-aggregated atomics.
+__device__ unsigned long long g_root_stats[8];
+__device__ __forceinline__ void root_stat(int i, bool c) {
+  const unsigned long long m = __ballot(c);
+  if (m && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
+    atomicAdd(&g_root_stats[i], (unsigned long long)__popcll(m));
+}
+#define FS_ROOT_STAT(i, c) root_stat(i, c)
+#else
+#define FS_ROOT_STAT(i, c) \
+  do {                     \
+  } while (0)
+#endif
+
 // The mesh-root cull of MeshBvhNode::Trace (mesh.cpp:79-83): true when the
 // reference would NOT skip the mesh (ray_intersect_bounds hits and its param
 // is <= best). Slab times use v_rcp (relative error < 3e-7 against the
@@ -205,10 +267,114 @@ __device__ __forceinline__ bool ref_bounds_hit(f3 mn, f3 mx, const Ray& r, bool 
 // fnear and ffar close, the decision is unsure only when one of those pairs
 // is close too (FS_ROOT_PAIRS). A flat box (a wall, a quad light: n_i = f_i)
 // no longer takes the exact path wherever it is hit: C2 +5.7 %, C4 +3.4 %.
-__device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best) {
+__device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best,
+                                               const Slopes* seg = nullptr) {
 #ifdef FS_MEAS_ROOT_ALL  // measurement builds only: every mesh root visited (frames differ)
   return !zl || in_bounds(mn, mx, r.start);
 #endif
+#if FS_ROOT_BF
+  // The same decisions as below, as one straight-line mask computation: every
+  // certain outcome (the exact tests, and the magnitude tests away from their
+  // thresholds) folds into sure_miss, and only a lane that is neither certain
+  // nor a zero-length / both-ends-inside case branches to the reference's
+  // divisions. A slab parallel to the segment sends the lane there too (never
+  // seen on the bench scenes: |v_i| < 1e-5 over a whole segment).
+  const bool si = in_bounds(mn, mx, r.start);
+  const bool both = si && in_bounds(mn, mx, r.stop);
+  const f3 s = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
+  bool par;
+  float rx, ry, rz;
+  if (FS_ROOT_HOIST && seg) {
+    // the segment's slopes, negated for the reversed segment (e - s = -(stop -
+    // start) exactly); |v_i| < 1e-5 (or a zero-length / tiny-substituted
+    // axis) shows as a slope of magnitude >= 1e5: the reference's path
+    par = fmaxf(fmaxf(fabsf(seg->ix), fabsf(seg->iy)), fabsf(seg->iz)) >= 99990.0f;
+    rx = si ? -seg->ix : seg->ix;
+    ry = si ? -seg->iy : seg->iy;
+    rz = si ? -seg->iz : seg->iz;
+  } else {
+    const f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
+    const f3 v = e - s;
+    par = cmp_eps(v.x, 0.0f, kEpsilon) || cmp_eps(v.y, 0.0f, kEpsilon) || cmp_eps(v.z, 0.0f, kEpsilon);
+    rx = __builtin_amdgcn_rcpf(v.x);
+    ry = __builtin_amdgcn_rcpf(v.y);
+    rz = __builtin_amdgcn_rcpf(v.z);
+  }
+  const float ax = (mn.x - s.x) * rx, bx = (mx.x - s.x) * rx;
+  const float ay = (mn.y - s.y) * ry, by = (mx.y - s.y) * ry;
+  const float az = (mn.z - s.z) * rz, bz = (mx.z - s.z) * rz;
+  const float n0 = fminf(ax, bx), f0 = fmaxf(ax, bx), n1 = fminf(ay, by), f1 = fmaxf(ay, by);
+  const float n2 = fminf(az, bz), f2 = fmaxf(az, bz);
+  const float fnear = fmaxf(fmaxf(n0, n1), n2), ffar = fminf(fminf(f0, f1), f2);
+#if FS_ROOT_TOL
+  // Margins from the error bound: a slab time here is (lo - s) * rcp(v), the
+  // reference's is the IEEE quotient of the same difference; v_rcp is within
+  // 1 ulp, so the two differ by at most 2.4e-7 |t| (1 ulp + two roundings).
+  // fnear, ffar (min/max of such times) carry the same bound, 1 - fnear adds
+  // at most 6e-8 (exact for fnear in [0.5, 2]); the margins below are 4x that.
+  auto close = [](float a, float b) { return fabsf(a - b) <= 1e-6f * (fabsf(a) + fabsf(b)); };
+  const float tol2 = 1e-6f, tol3 = 1e-6f * fabsf(fnear) + 1e-7f;
+#else
+  auto close = [](float a, float b) { return fabsf(a - b) <= 1e-5f * (fabsf(a) + fabsf(b)); };
+  const float tol2 = 1e-5f, tol3 = 1e-5f;
+#endif
+  bool u1 = close(fnear, ffar);
+  if (u1)  // a flat box hit away from its edges stays certain (FS_ROOT_PAIRS)
+    u1 = close(n0, f1) || close(n0, f2) || close(n1, f0) || close(n1, f2) || close(n2, f0) || close(n2, f1);
+  const bool u2 = fabsf(fnear - 1.0f) <= tol2;
+  const float np = si ? 1.0f - fnear : fnear;
+  const bool u3 = fabsf(np - best) <= tol3;
+  const bool sure_miss = !par && ((ffar < 0) || (fnear < 0) || (!u1 && fnear > ffar) || (!u2 && fnear > 1.0f) ||
+                                  (!u3 && np > best));
+  bool visit = zl ? si : (both || !sure_miss);
+  FS_ROOT_STAT(0, true);
+  FS_ROOT_STAT(1, !zl && !both && !sure_miss && (par || u1 || u2 || u3));
+  FS_ROOT_STAT(2, !zl && !both && !sure_miss && par);
+  FS_ROOT_STAT(3, !zl && !both && !sure_miss && u1);
+  FS_ROOT_STAT(4, !zl && !both && !sure_miss && u2);
+  FS_ROOT_STAT(5, !zl && !both && !sure_miss && u3);
+  FS_ROOT_STAT(6, !zl && !both && !sure_miss && si);
+#ifndef FS_MEAS_NO_EXACT  // measurement builds only: no exact fallback (frames may differ)
+  if (!zl && !both && !sure_miss && (par || u1 || u2 || u3)) {
+#if FS_ROOT_LITE
+    // ray_intersect_bounds' worker (intersect.cpp:490-597) on the same
+    // segment, straight-line: per slab the entry and exit times as the
+    // reference's IEEE quotients ((lo - s) / v and (hi - s) / v, ordered by the
+    // sign of v: division by a positive v is monotone, so the reference's
+    // swap picks the same operand), a parallel slab (cmp_eps(v, 0)) as no
+    // bound or, start outside it, a miss.
+    const f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
+    const f3 w = e - s;
+    auto entry = [&](float sa, float va, float lo, float hi) { return ((va > 0.0f ? lo : hi) - sa) / va; };
+    float en = fmaxf(fmaxf(entry(s.x, w.x, mn.x, mx.x), entry(s.y, w.y, mn.y, mx.y)), entry(s.z, w.z, mn.z, mx.z));
+    bool hit;
+    if (par || u1) {  // the exit times (and a parallel slab's test) decide too
+      bool out = false;
+      float ex = kInfinity;
+      en = -kInfinity;
+      auto slab = [&](float sa, float va, float lo, float hi) {
+        const bool p = cmp_eps(va, 0.0f, kEpsilon);
+        out |= p && (sa < lo || sa > hi);
+        en = p ? en : fmaxf(en, entry(sa, va, lo, hi));
+        ex = p ? ex : fminf(ex, ((va > 0.0f ? hi : lo) - sa) / va);
+      };
+      slab(s.x, w.x, mn.x, mx.x);
+      slab(s.y, w.y, mn.y, mx.y);
+      slab(s.z, w.z, mn.z, mx.z);
+      hit = !out && !(en > ex) && !(ex < 0 || en < 0 || en > 1);
+    } else {  // only fnear ~ 1 or param ~ best was unsure: every other test is settled
+      hit = !(en > 1);
+    }
+    const float pe = si ? 1.0f - en : en;
+    visit = hit && !(pe > best);
+#else
+    float pe;
+    visit = ref_ray_bounds(mn, mx, r, zl, pe) && !(pe > best);
+#endif
+  }
+#endif
+  return visit;
+#else
   bool si = in_bounds(mn, mx, r.start);
   if (zl) return si;                                 // param 0 (intersect.cpp:604-616)
   if (si && in_bounds(mn, mx, r.stop)) return true;  // param 0 (:621-630)
@@ -253,6 +419,7 @@ __device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool 
   if (!unsure) return true;
   float pe;
   return ref_ray_bounds(mn, mx, r, zl, pe) && !(pe > best);
+#endif
 }
 
 // intersect.cpp:96-129 + 146-177: planar map, then barycentrics.
@@ -854,31 +1021,6 @@ __device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t fir
   }
 }
 
-// Per-ray slab constants of the BVH walks, computed once per segment. A
-// zero-length ray (a point test at the leaves) walks with a 1e-20 slope per
-// axis: every box that contains the start passes the slab test (entry <= 0 <=
-// exit), so the cull stays a superset of the point-in-box test without a
-// per-node branch. v_rcp (about 1 ulp) instead of IEEE division: the slab
-// test is a conservative cull whose t margins (1e-6 absolute, 2e-6 relative)
-// and box padding (4e-5 x scale) dwarf a 1e-7 relative error in the slopes.
-struct Slopes {
-  float ix, iy, iz, ox, oy, oz;
-};
-__device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) {
-  const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny || zl ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny || zl ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny || zl ? copysignf(tiny, r.dir.z) : r.dir.z;
-  Slopes sl;
-  sl.ix = __builtin_amdgcn_rcpf(dx);
-  sl.iy = __builtin_amdgcn_rcpf(dy);
-  sl.iz = __builtin_amdgcn_rcpf(dz);
-  sl.ox = -r.start.x * sl.ix;
-  sl.oy = -r.start.y * sl.iy;
-  sl.oz = -r.start.z * sl.iz;
-  return sl;
-}
-
 // SUSP: when at most `thr` lanes are still walking while other live lanes of
 // the wave wait, the walkers park (state to *ws) and return true; the wave
 // moves on and they resume from *ws in a later iteration (same operations in
@@ -1443,7 +1585,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   const uint32_t me = sw * kBlock + (threadIdx.x & (kBlock - 1));  // POOL: this lane's slot
   bool park = false;
 #if FS_HOIST_SLOPES
-  const Slopes sl = walk_slopes(r, zl);  // once per segment, not once per mesh walk
+  const Slopes sl = FS_ROOT_HOIST ? seg_slopes(r, zl) : walk_slopes(r, zl);  // once per segment
   const Slopes* slp = &sl;
 #else
   const Slopes* slp = nullptr;
@@ -1466,7 +1608,8 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       if (!H.i2) continue;
       uint64_t t0 = FS_TICK();
       const bool resume_here = PARK && resuming && (uint32_t)ws->oi == oi;
-      bool visit = resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t);
+      bool visit =
+          resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t, slp);
       uint64_t t1 = FS_TICK();
       if (H.i3) {  // a small mesh: its faces, no walk (never parks)
         if (visit)
@@ -3229,6 +3372,14 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->small_tri_loads = c.small_tri_loads;
   out->lane_object_loads = c.lane_object_loads;
 #ifdef FS_PHASE_PROF
+  {
+    unsigned long long rs[8] = {};
+    if (hipMemcpyFromSymbol(rs, HIP_SYMBOL(dev::g_root_stats), sizeof(rs)) == hipSuccess)
+      std::fprintf(stderr, "[fs root] culls %llu exact %llu (par %llu pair %llu near-1 %llu near-best %llu; start inside %llu)\n",
+                   rs[0], rs[1], rs[2], rs[3], rs[4], rs[5], rs[6]);
+    const unsigned long long zero[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(dev::g_root_stats), zero, sizeof(zero));
+  }
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "
                "shade %llu unwind %llu - iters %llu total %llu\n",

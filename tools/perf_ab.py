@@ -54,6 +54,9 @@ def main():
                     ref = img
                 elif not np.array_equal(img, ref):
                     print(f"  !! variant {v} output differs from variant {variants[0]}", flush=True)
+        if os.environ.get("PERF_AB_HASH"):  # frames of different builds compared across processes
+            import hashlib
+            print(f"{name} frame md5 {hashlib.md5(ref.tobytes()).hexdigest()}", flush=True)
         for v in variants:
             ms = np.median(res[v])
             print(f"{name} variant {v}: median {ms:.1f} ms  {W*H*spp/ms/1e3:.1f} Msamples/s  (min {min(res[v]):.1f})",
