@@ -60,6 +60,9 @@
 #endif
 // Object loop: each record's first 64 B as one scalar load (1) or each field
 // where it is first used (0, A/B)
+#ifndef FS_ROWS_LANE  // HBM shading rows lane-major, the backward pass's c values in two loads (1)
+#define FS_ROWS_LANE 1
+#endif
 #ifndef FS_ROOT_BF  // mesh-root cull as straight-line masks (1) or early returns (0)
 #define FS_ROOT_BF 1
 #endif
@@ -773,7 +776,17 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
 // SELECTS: Material::Sample as straight-line selects (the kernels without
 // parked walks: C2 +2.3 %, C3 +0.9 %) or as a per-kind switch (the parked-walk
 // kernel: the selects cost C4 0.9 %).
-template <bool TEX = false, bool MMAT = false, bool SELECTS = false>
+// LROWS: the rows are lane-major ([lane][level], HBM rows of the walk
+// kernels): the path's eight c values arrive in two 16-B loads before the
+// first level, and the level loop runs unrolled over wave-uniform levels
+// (constant register indices), so only the hot material records stay on each
+// level's critical path, not an L2 round trip to the row.
+template <bool LROWS>
+__device__ __forceinline__ uint32_t row_off(uint32_t level, uint32_t lane, bool hi, uint32_t stride = kBlock) {
+  if (LROWS) return (hi ? kMaxDepth * kBlock : 0u) + lane * kMaxDepth + level;
+  return ((hi ? kMaxDepth : 0u) + level) * stride + lane;
+}
+template <bool TEX = false, bool MMAT = false, bool SELECTS = false, bool LROWS = false>
 __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const MatTrail<MMAT>& mats,
                                      const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
                                      int stride = kBlock, uint32_t lane = 0,
@@ -784,17 +797,32 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
   const fs_material* mp = &S.materials[mats.get(top)];
   int32_t kind = mp->kind;
   f3 dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
-  float c = *at_byte(cv, ((uint32_t)top * (uint32_t)stride + lane) * 4u);
-  for (int k = top; k >= 0; --k) {
+  float cs[kMaxDepth];
+  float c = 0.0f;
+  if constexpr (LROWS) {
+    static_assert(kMaxDepth == 8, "two 16-B loads per lane");
+    const float4* q = reinterpret_cast<const float4*>(at_byte(cv, lane * (kMaxDepth * 4u)));
+    const float4 a = q[0], b = q[1];
+    cs[0] = a.x, cs[1] = a.y, cs[2] = a.z, cs[3] = a.w, cs[4] = b.x, cs[5] = b.y, cs[6] = b.z, cs[7] = b.w;
+    // (the specular terms of a Ceramic/Glow path as two more loads: C3 -7.6 %,
+    // C4 -2.4 %, spills 60 -> 76 B/lane; they stay loads at their level)
+  } else {
+    c = *at_byte(cv, ((uint32_t)top * (uint32_t)stride + lane) * 4u);
+  }
+#pragma unroll
+  for (int lv = (LROWS ? (int)kMaxDepth - 1 : 0); lv >= 0; --lv) {
+   const int k0 = LROWS ? lv : top;
+   if (LROWS && lv > top) continue;
+   for (int k = k0; k >= (LROWS ? lv : 0); --k) {
     const fs_material& m = *mp;
     const int32_t kk = kind;
     const f3 dk = dif;
-    const float ck = c;
+    const float ck = LROWS ? cs[LROWS ? lv : 0] : c;
     if (k > 0) {  // next level's loads, in flight while this level is applied
       mp = &S.materials[mats.get(k - 1)];
       kind = mp->kind;
       dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
-      c = *at_byte(cv, ((uint32_t)(k - 1) * (uint32_t)stride + lane) * 4u);
+      if (!LROWS) c = *at_byte(cv, ((uint32_t)(k - 1) * (uint32_t)stride + lane) * 4u);
     }
     f3 sd = dk;  // SampleDiffuse (material.cpp:108-126)
     if (TEX && m.texture >= 0) {
@@ -811,7 +839,7 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
       const bool metal = kk == FS_MAT_METAL, cer = kk == FS_MAT_CERAMIC || kk == FS_MAT_GLOW;
       float wa = 0.0f, wb = 0.0f;  // the two weights of Metal and Ceramic
       if (metal || cer) {
-        wa = metal ? m.roughness : *at_byte(cv, ((kMaxDepth + (uint32_t)k) * (uint32_t)stride + lane) * 4u);
+        wa = metal ? m.roughness : *at_byte(cv, row_off<LROWS>((uint32_t)k, lane, true, (uint32_t)stride) * 4u);
         wb = (float)(1.0 - (double)wa);
       }
       const f3 t = (mirrorish ? dk : sd) * L;  // L*dif is dif*L bit for bit
@@ -850,7 +878,7 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
           break;
         case FS_MAT_CERAMIC:
         case FS_MAT_GLOW: {
-          const float ds = *at_byte(cv, ((kMaxDepth + (uint32_t)k) * (uint32_t)stride + lane) * 4u);
+          const float ds = *at_byte(cv, row_off<LROWS>((uint32_t)k, lane, true, (uint32_t)stride) * 4u);
           f3 dc = (sd * L) * ck;
           L = L * ds + dc * (float)(1.0 - (double)ds);
           if (kk == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
@@ -867,6 +895,7 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
           break;
       }
     }
+   }
   }
   // engine.cpp:147-151 (kind holds level 0's: the loop ends on it)
   if (length(L) > 10.0f && kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
@@ -2043,6 +2072,7 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
   // POOL: the shading waves' rows in LDS too (the walk stack and the pool
   // take 12 KiB of a 4-wave workgroup's 26 KiB share at 6 waves per SIMD).
   constexpr bool kLdsRows = NOWALK || (POOL && FS_POOL_LDS_ROWS);
+  constexpr bool kLaneRows = FS_ROWS_LANE && !kLdsRows && SUSP;  // HBM rows lane-major (unwind's LROWS)
   __shared__ uint32_t stk_all[NOWALK ? 1 : kTraversalStack * kBlock];
   __shared__ float2 lvl_lds[kLdsRows ? (POOL ? kPoolWaves - 1 : 1) * kMaxDepth * kBlock : 1];
   // POOL: workgroups of kPoolWaves waves; wave 0 walks for the others (walk_service)
@@ -2320,9 +2350,9 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
           ds = pow50(dot(hv, nn));
         }
 #ifndef FS_MEAS_NO_LVL  // measurement builds only (tools/gpu_writes.sh): the write streams one by one
-        *at_byte(reinterpret_cast<float*>(lvl), (depth * kBlock + lane) * 4u) = c;  // [level][lane]
-        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)  // [kMaxDepth + level][lane]
-          *at_byte(reinterpret_cast<float*>(lvl), ((kMaxDepth + depth) * kBlock + lane) * 4u) = ds;
+        *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, false) * 4u) = c;
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)
+          *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, true) * 4u) = ds;
 #endif
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
@@ -2366,7 +2396,7 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
         lp0 = mk3(b.x, b.y, b.z);
       }
 #ifndef FS_MEAS_NO_UNWIND  // measurement builds only: no backward pass (frames differ)
-      L = unwind<TEX, MMAT, !SUSP>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
+      L = unwind<TEX, MMAT, !SUSP, kLaneRows>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
 #else
       L.x += (float)top + p0.x + lp0.x;
 #endif
