@@ -240,8 +240,9 @@ __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) { return wa
 __device__ __forceinline__ Slopes seg_slopes(const Ray& r, bool zl) { return walk_slopes(r, zl, r.stop - r.start); }
 
 
-#ifdef FS_PHASE_PROF
-// Mesh-root cull outcomes (profiling build): lanes tested, lanes sent to the
+#if defined(FS_PHASE_PROF) && defined(FS_ROOT_STATS)
+// Mesh-root cull outcomes (profiling build with -DFS_ROOT_STATS: seven
+// atomics per cull, so its phase split is not the product's): lanes tested, lanes sent to the
 // reference's divisions, and why (parallel slab, fnear~ffar with a close
 // cross-slab pair, fnear~1, param~best). Wave-aggregated atomics.
 __device__ unsigned long long g_root_stats[8];
@@ -3402,6 +3403,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->small_tri_loads = c.small_tri_loads;
   out->lane_object_loads = c.lane_object_loads;
 #ifdef FS_PHASE_PROF
+#ifdef FS_ROOT_STATS
   {
     unsigned long long rs[8] = {};
     if (hipMemcpyFromSymbol(rs, HIP_SYMBOL(dev::g_root_stats), sizeof(rs)) == hipSuccess)
@@ -3410,6 +3412,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
     const unsigned long long zero[8] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(dev::g_root_stats), zero, sizeof(zero));
   }
+#endif
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "
                "shade %llu unwind %llu - iters %llu total %llu\n",
