@@ -800,6 +800,8 @@ __device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const Mat
   f3 dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
   float cs[kMaxDepth];
   float c = 0.0f;
+  // (Metal's roughness and Ceramic's specular term loaded one level ahead
+  // with the material: C3 -2.4 %, C4 -1.6 %, profiles/r03/ab_unwind_pipe.log)
   if constexpr (LROWS) {
     static_assert(kMaxDepth == 8, "two 16-B loads per lane");
     const float4* q = reinterpret_cast<const float4*>(at_byte(cv, lane * (kMaxDepth * 4u)));
@@ -2970,7 +2972,7 @@ int fs_options_default(fs_options* o) {
   if (!o) return fail(FS_ERR_INVALID, "null options");
   *o = fs_options{};
   o->schedule = FS_SCHEDULE_AUTO;
-  o->park_lanes = 10;       // C4 (1 M-face blob): 10-12 best
+  o->park_lanes = 12;       // C4 (1 M-face blob): 12 best on the round-3 build (10: -0.5 %, 14: -0.1 %)
   o->park_lanes_small = 6;  // C3 (38 k and 209 k-face meshes): 4-6 best
   o->park_min_tris = kParkMinTris;
   o->lds_rows = 1;

@@ -241,7 +241,7 @@ typedef enum fs_schedule {
 typedef struct fs_options {
   int32_t schedule;            /* fs_schedule (AUTO) */
   uint32_t park_lanes;         /* PARKED: park when at most this many lanes still walk a mesh of
-                                  >= 2^19 triangles (10) */
+                                  >= 2^19 triangles (12) */
   uint32_t park_min_tris;      /* meshes whose walks may park (32768); read at upload */
   uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (16) */
   uint32_t groups;             /* sample groups per launch (0). 0 = automatic: with persist = 1

@@ -45,7 +45,7 @@ def test_options_defaults_and_validation_without_device():
     (checked by fs_prepare_digest, which needs no device)."""
     o = fsamd.options()
     d = fsamd.options_dict(o)
-    assert d == {"schedule": 0, "park_lanes": 10, "park_min_tris": 1 << 15, "samples_per_block": 16, "groups": 0,
+    assert d == {"schedule": 0, "park_lanes": 12, "park_min_tris": 1 << 15, "samples_per_block": 16, "groups": 0,
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
                  "small_mesh_tris": 16, "park_lanes_small": 6,
