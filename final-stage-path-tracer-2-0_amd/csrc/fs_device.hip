@@ -25,11 +25,11 @@
 #ifndef FS_FLAT_LEAF  // leaf tests one triangle per trip over both leaves (A/B)
 #define FS_FLAT_LEAF 1
 #endif
-// Wave priority inside BVH walks (s_setprio): waves in a walk issue first,
-// so the dependent node fetches of the latency-bound walks start sooner
-// (C2 +1.3 %, C3 +0.8 %, C4 neutral; 1 and 3 measure the same; 0 = off)
+// Wave priority inside BVH walks (s_setprio 1..3; 0 = off). Round 1 measured
+// C2 +1.3 %, C3 +0.8 %, C4 neutral for 1. On the round-3 build it is off:
+// C4 +1.1 %, C3 +0.3 %, C2 +-0 against 1 (3 as 1; profiles/r03/ab_sched.log).
 #ifndef FS_TRAV_PRIO
-#define FS_TRAV_PRIO 1
+#define FS_TRAV_PRIO 0
 #endif
 // BVH-walk slab constants once per segment (1) or once per mesh walk (0, A/B)
 #ifndef FS_HOIST_SLOPES

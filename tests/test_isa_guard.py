@@ -21,8 +21,10 @@ LIMITS = {
     # lane-major rows and the unrolled backward pass (C4 +3.5 % all the same,
     # profiles/r03/ab_lrows.log)
     "render_kernel_lean<false, 6, false, true, false, false, false, false>": (60, 21, 80),
-    # LEAN schedule: scenes with BVH walks and no large mesh
-    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (16, 12, 80),
+    # LEAN schedule: scenes with BVH walks and no large mesh. 16 -> 20 B/lane
+    # without the traversal s_setprio (FS_TRAV_PRIO 0: C4 +1.1 %, C3 +0.3 % on
+    # the parked-walk kernel, profiles/r03/ab_sched.log; no bench config runs LEAN)
+    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (20, 12, 80),
     # LEAN without walks (NOWALK: every mesh small, shading rows in LDS, 8 waves
     # per SIMD): C1 and C2. 32 -> 44 B/lane with the straight-line mesh-root
     # cull on the segment's slopes (C2 +6.7 % all the same, profiles/r03/ab_root_tol.log)
