@@ -18,6 +18,7 @@ rendezvous.FileGroup, files in a directory the launcher's ranks share.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -33,6 +34,7 @@ sys.path.insert(0, PKG)
 import fsamd  # noqa: E402
 import rendezvous  # noqa: E402
 import scenes  # noqa: E402
+import tiles  # noqa: E402
 
 # The HIP layer (libfsgpu.so + libfshost.so) is loaded here, first.
 fsamd.gpu_lib()
@@ -56,12 +58,13 @@ WORKLOADS = {
 # one material record (76 B) + one normal-table entry (16 B); per sample 12 B
 # of radiance.
 S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 92, 12
-# tools/cpu_calibration.py, survey container, 8 threads, against the reference rates
-# of SURVEY.md §6 [probe]
-CPU_CALIBRATION = ("restatement/reference rate on the survey's probe scenes (8 threads, build container, DESIGN "
-                   "§6): C1 0.99-1.18, 250k probe 0.55-0.64, C4 0.65-0.66 this session (C4 1.03 in round 2's): "
-                   "within a factor of about 2 either way; the reference cannot be built here for a same-machine "
-                   "calibration")
+# tools/cpu_calibration.py on SURVEY Appendix A's own probe scenes (the C1 room + a UV-sphere blob,
+# scenes.write_probe), 8 threads in the build container, against the reference rates and octree
+# counts SURVEY records for them
+CPU_CALIBRATION = ("oracle vs reference on SURVEY's probe scenes (8 threads, build container, DESIGN §6): "
+                   "250k probe rate x1.40 at 3.50 vs 5.02 segments/sample and 145 vs 137 triangle tests per "
+                   "segment, i.e. x1.03 per triangle test; 1M probe x1.09 at 3.37 vs 5.05 and 483 vs 451, "
+                   "x0.78 per triangle test; the reference cannot be built here for a same-machine run")
 
 
 def parse():
@@ -87,6 +90,22 @@ def parse():
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def build_id(so_path=None):
+    """Identity of the libfsgpu.so build this process runs: the SHA-256 of its
+    gfx950 code object (every kernel's machine code and metadata). A PMC
+    summary under profiles/ carries the same digest (tools/pmc_summary.py);
+    make_roofline replays one only onto the build it was measured on."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_guard
+
+    so_path = so_path or fsamd.gpu_lib_path()
+    try:
+        return hashlib.sha256(isa_guard.code_object(so_path)).hexdigest()
+    except (OSError, ValueError) as e:
+        log(f"build id of {so_path}: {e}")
+        return None
 
 
 def main():
@@ -178,6 +197,9 @@ def run(args, rank, world, local_rank, group):
         rows = group.allgather([elapsed_local, sum(kernel_ms) / len(kernel_ms), sum(gather_ms) / len(gather_ms)])
         per_rank = per_rank_stats(rows, rccl_ranks)
         elapsed = max(row[0] for row in rows)
+        # the last step's gathered frame, checked tile set by tile set (outside the timed region)
+        per_rank.update(gather_check(group, rank, world, lambda k: r.pack(
+            frame, fsamd.render_params(W, H, spp, tile_offset=k, tile_stride=world)).tobytes()))
 
     # ---- roofline of the trace kernel: algorithmic bytes from a counted launch
     cf = r.frame(W, H)
@@ -185,7 +207,8 @@ def run(args, rank, world, local_rank, group):
     r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
     c = r.counters()
     cf.close()
-    roofline = make_roofline(args.scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp)
+    roofline = make_roofline(args.scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp,
+                             build_id())
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -194,6 +217,27 @@ def run(args, rank, world, local_rank, group):
     if rank == 0:
         out = make_record(args, world, elapsed, stats, roofline, cpu, per_rank)
         print(json.dumps(out), flush=True)
+
+
+def tile_digest(pack_bytes):
+    """Digest of one rank's tile set in the 40-B/pixel exchange format."""
+    return hashlib.sha256(pack_bytes).hexdigest()[:16]
+
+
+def gather_check(group, rank, world, pack_fn):
+    """Verifies the gathered frame of an N > 1 step. pack_fn(k) packs tile set
+    k (the tiles t with t % world == k, fs_frame_pack's format) from this
+    rank's frame: each rank digests its own tiles as it rendered them, the
+    digests are allgathered, and rank 0 digests every rank's tiles again
+    from the frame the RCCL gather assembled. gather_ok says they all
+    match; rank 0 returns the fields, the other ranks an empty dict."""
+    own = tile_digest(pack_fn(rank))
+    digests = [d.decode() for d in group.allgather_bytes(own.encode())]
+    if rank != 0:
+        return {}
+    root = [tile_digest(pack_fn(k)) for k in range(world)]
+    bad = [k for k in range(world) if root[k] != digests[k]]
+    return {"gather_ok": not bad, "tile_digests": digests, "gather_mismatch_ranks": bad}
 
 
 def per_rank_stats(rows, rccl_ranks):
@@ -207,20 +251,40 @@ def per_rank_stats(rows, rccl_ranks):
             "render_imbalance": round(max(render) / max(min(render), 1e-9), 4)}
 
 
-def pmc_record(scene, W, H, kernel_name):
-    """The committed PMC summary of this kernel on this workload (tools/gpu_pmc.sh +
-    tools/pmc_summary.py), or None: the run replays it, it does not measure it."""
+def pmc_record(scene, W, H, kernel_name, build):
+    """The committed PMC summary of this kernel on this workload (tools/gpu_run.sh
+    pmc + tools/pmc_summary.py), or None and the reason: the run replays it,
+    it does not measure it, and only onto the build it was measured on (the
+    code-object digest both carry; a summary of another build is refused even
+    when the kernel's template name is the same)."""
     path = os.path.join("profiles", f"pmc_{scene}_{W}x{H}.json")
     try:
         pm = json.load(open(os.path.join(ROOT, path)))
     except (OSError, ValueError):
-        return None, path
+        return None, path, "no PMC summary for this workload"
     if kernel_name not in pm.get("kernel", ""):
-        return None, path
-    return pm, path
+        return None, path, f"PMC summary is of another kernel ({pm.get('kernel')})"
+    if not build or pm.get("code_object_sha256") != build:
+        return None, path, (f"PMC summary is of build {str(pm.get('code_object_sha256'))[:12]}, "
+                            f"this run is {str(build)[:12]}")
+    return pm, path, None
 
 
-def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp):
+def roofline_bound(frac_traffic, valu_issue_frac, wait_any_frac):
+    """What bounds the kernel, from MEASURED fractions (the PMC summary of
+    this build): HBM when its measured traffic rate is the larger fraction of
+    its peak, VALU when the issue rate is; "latency" when neither reaches half
+    of its peak while waves wait on dependencies for more than 40 % of their
+    cycles. Without measurements: None (the line then says "hbm", the
+    roofline frac is priced against, and bound_source says it is unmeasured)."""
+    if frac_traffic is None or valu_issue_frac is None:
+        return None
+    if max(frac_traffic, valu_issue_frac) < 0.5 and (wait_any_frac or 0.0) > 0.4:
+        return "latency"
+    return "valu" if valu_issue_frac > frac_traffic else "hbm"
+
+
+def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp, build=None):
     bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * (c["tri_tests"] + c["small_tri_loads"])
                         + S_OBJ * (c["object_loads"] + c.get("lane_object_loads", 0))
                         + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
@@ -229,9 +293,10 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
     per_launch_bytes = bytes_per_sample * owned_samples / launches
     achieved = per_launch_bytes / avg_launch_s / 1e9
     hbm_frac = achieved / HBM_PEAK_GBS
-    pm, pm_path = pmc_record(scene, W, H, kernel_name)
+    pm, pm_path, refused = pmc_record(scene, W, H, kernel_name, build)
     traffic = None
     valu = None
+    src = pm_path + " (same build: replayed per sample onto this run's launch time, not measured by this run)"
     if pm and pm.get("hbm_bytes_per_sample"):
         traffic = round(pm["hbm_bytes_per_sample"] * owned_samples / launches)
     if pm and pm.get("valu_insts_per_sample") and pm.get("clock_ghz"):
@@ -246,19 +311,29 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
         insts = pm["valu_insts_per_sample"] * samples_launch
         issue = insts * 2 / (1024 * clock * avg_launch_s)
         lane_ops = insts * 64 * pm["valu_lane_util"]
-        valu = {"valu_issue_frac": round(issue, 4), "valu_busy_rocprof": pm.get("valu_busy"),
-                "valu_lane_util": pm["valu_lane_util"],
+        valu = {"valu_issue_frac": round(issue, 4), "valu_lane_util": pm["valu_lane_util"],
                 "valu_lane_op_frac": round(lane_ops / avg_launch_s / VALU_LANE_OPS_PEAK, 4),
                 "valu_insts_per_sample": pm["valu_insts_per_sample"], "clock_ghz": pm["clock_ghz"],
-                "wait_any_frac": pm.get("wait_any_frac"),
-                "source": pm_path + " (replayed per sample, not measured by this run)"}
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(hbm_frac, 4), "traffic": traffic,
-            "traffic_source": pm_path + " (replayed per sample, not measured by this run)" if traffic else None,
+                "wait_any_frac": pm.get("wait_any_frac"), "source": src}
+    frac_traffic = round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
+    bound = roofline_bound(frac_traffic, valu["valu_issue_frac"] if valu else None,
+                           valu["wait_any_frac"] if valu else None)
+    roof = {"bound": bound or "hbm",
+            "bound_source": ("measured: PMC traffic fraction, VALU issue fraction and wave wait share of this "
+                             "build (roofline_bound)") if bound else
+                            f"unmeasured ({refused or 'PMC summary incomplete'}): the HBM roofline frac is priced on",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(hbm_frac, 4),
+            "frac_source": "algorithmic bytes (SURVEY 8d byte model x this run's device counters) per launch / "
+                           "HIP-event launch time",
+            "traffic": traffic,
+            "traffic_source": src if traffic else None,
             # the same launch time against the PMC-measured bytes (FETCH x2 + WRITE per launch)
             "traffic_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic else None,
-            "frac_traffic": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "frac_traffic": frac_traffic,
             "valu": valu,
+            "pmc_replay_refused": refused,
+            "build": build,
             "kernel": kernel_name, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
             "launches_per_step": launches, "spp_per_launch": launch_spp,
             "bytes_per_sample": round(bytes_per_sample, 1),
@@ -268,8 +343,6 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
             "object_loads_per_sample": round(c["object_loads"] / max(c["samples"], 1), 3),
             "small_tri_loads_per_sample": round(c["small_tri_loads"] / max(c["samples"], 1), 3),
             "prim_tests_per_sample": round(c["prim_tests"] / max(c["samples"], 1), 3)}
-    if valu and valu["valu_issue_frac"] > hbm_frac:
-        roof["bound"] = "valu"  # the larger of the two fractions names the nearer resource
     return roof
 
 

@@ -22,65 +22,14 @@
 #include "fs_scene.h"
 #include "fs_trace.h"
 
-#ifndef FS_FLAT_LEAF  // leaf tests one triangle per trip over both leaves (A/B)
-#define FS_FLAT_LEAF 1
-#endif
-// Wave priority inside BVH walks (s_setprio 1..3; 0 = off). Round 1 measured
-// C2 +1.3 %, C3 +0.8 %, C4 neutral for 1. On the round-3 build it is off:
-// C4 +1.1 %, C3 +0.3 %, C2 +-0 against 1 (3 as 1; profiles/r03/ab_sched.log).
-#ifndef FS_TRAV_PRIO
-#define FS_TRAV_PRIO 0
-#endif
-// BVH-walk slab constants once per segment (1) or once per mesh walk (0, A/B)
-#ifndef FS_HOIST_SLOPES
-#define FS_HOIST_SLOPES 1
-#endif
-// Slab exit clamp to the walk's t limit as a signed-integer min on the float
-// bits (1) instead of fminf (0, A/B): the limit is positive, so the integer
-// order is the float order for every finite exit, and v_min_f32 needed the
-// loop-carried limit re-canonicalised on every node trip.
-#ifndef FS_SLAB_IMIN
-#define FS_SLAB_IMIN 1
-#endif
-// Mesh-root cull: the rcp slab decision is redone with the reference's
-// divisions only when a cross-slab pair of entry/exit params is close (1), or
-// whenever the entry and exit params are close (0, A/B: every hit on a flat
-// box, e.g. a Cornell wall, took the exact path).
-#ifndef FS_ROOT_PAIRS
-#define FS_ROOT_PAIRS 1
-#endif
-// Radiance rows of a block: [sample][pixel][rgb], one 12-B store per sample
-// (1), or [rgb][sample][pixel], three 4-B stores 1 KiB apart (0, A/B). The
-// rows are written once, by lanes that finish in different iterations, so
-// their lines leave L2 partly written: measured write traffic 50 B per 12-B
-// sample with the planar layout.
-// POOL kernel: the shading waves' per-bounce rows in LDS (1) or HBM (0, A/B)
-#ifndef FS_POOL_LDS_ROWS
-#define FS_POOL_LDS_ROWS 1
-#endif
-// Object loop: each record's first 64 B as one scalar load (1) or each field
-// where it is first used (0, A/B)
-#ifndef FS_ROWS_LANE  // HBM shading rows lane-major, the backward pass's c values in two loads (1)
-#define FS_ROWS_LANE 1
-#endif
-#ifndef FS_ROOT_BF  // mesh-root cull as straight-line masks (1) or early returns (0)
-#define FS_ROOT_BF 1
-#endif
-#ifndef FS_ROOT_TOL  // FS_ROOT_BF: margins of the fast cull from its error bound (1) or 1e-5 (0)
-#define FS_ROOT_TOL 1
-#endif
-#ifndef FS_ROOT_LITE  // FS_ROOT_BF: the exact path as straight-line code (1) or ref_ray_bounds (0)
-#define FS_ROOT_LITE 1
-#endif
-#ifndef FS_ROOT_HOIST  // FS_ROOT_BF: the segment's slopes computed once for every mesh root (1)
-#define FS_ROOT_HOIST 1
-#endif
-#ifndef FS_OBJ_HEAD
-#define FS_OBJ_HEAD 1
-#endif
-#ifndef FS_RAD_XYZ
-#define FS_RAD_XYZ 1
-#endif
+// Round 4 pruned the compile-time A/B switches of rounds 1-3 to the settings
+// that ship (each one's measurement is in DESIGN.md §5 and §9): leaves tested
+// one triangle per wave trip, no wave priority in the walks, slab constants
+// once per segment, the integer-min exit clamp, the mesh-root cull as
+// straight-line masks with error-bound margins and a straight-line exact path,
+// lane-major HBM shading rows, object heads as one scalar load, 12-B radiance
+// records. The only remaining switch is FS_PHASE_PROF (the profiling build,
+// libfsgpu_prof.so).
 
 namespace fs {
 namespace dev {
@@ -232,7 +181,7 @@ __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl, f3 dir) {
   return sl;
 }
 __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) { return walk_slopes(r, zl, r.dir); }
-// The object loop's slopes (FS_ROOT_HOIST): from the segment stop - start, the
+// The object loop's slopes: from the segment stop - start, the
 // v of the reference's ray_intersect_bounds (intersect.cpp:531-597), so the
 // mesh-root culls reuse them (the reversed segment's slopes are their
 // negation, exactly); the walks cull with them as well (dir and stop - start
@@ -240,107 +189,50 @@ __device__ __forceinline__ Slopes walk_slopes(const Ray& r, bool zl) { return wa
 __device__ __forceinline__ Slopes seg_slopes(const Ray& r, bool zl) { return walk_slopes(r, zl, r.stop - r.start); }
 
 
-#if defined(FS_PHASE_PROF) && defined(FS_ROOT_STATS)
-// Mesh-root cull outcomes (profiling build with -DFS_ROOT_STATS: seven
-// atomics per cull, so its phase split is not the product's): lanes tested, lanes sent to the
-// reference's divisions, and why (parallel slab, fnear~ffar with a close
-// cross-slab pair, fnear~1, param~best). Wave-aggregated atomics.
-__device__ unsigned long long g_root_stats[8];
-__device__ __forceinline__ void root_stat(int i, bool c) {
-  const unsigned long long m = __ballot(c);
-  if (m && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
-    atomicAdd(&g_root_stats[i], (unsigned long long)__popcll(m));
-}
-#define FS_ROOT_STAT(i, c) root_stat(i, c)
-#else
-#define FS_ROOT_STAT(i, c) \
-  do {                     \
-  } while (0)
-#endif
-
 // The mesh-root cull of MeshBvhNode::Trace (mesh.cpp:79-83): true when the
 // reference would NOT skip the mesh (ray_intersect_bounds hits and its param
-// is <= best). Slab times use v_rcp (relative error < 3e-7 against the
-// reference's IEEE quotient) after the reference's exact subtraction, so all
-// sign tests are exact; a magnitude comparison within 1e-5 of its threshold
-// is redone with the reference's divisions. Exact by construction.
-// Per-slab entry/exit (a slab parallel to the segment: +-1e30, never close to
-// anything). The reference's test fnear > ffar is max(n_i) > min(f_j); for
-// i == j, n_i <= f_i holds exactly in both (the same product sorted, or one
-// product twice for a flat box), so only the cross-slab pairs can flip: with
-// fnear and ffar close, the decision is unsure only when one of those pairs
-// is close too (FS_ROOT_PAIRS). A flat box (a wall, a quad light: n_i = f_i)
-// no longer takes the exact path wherever it is hit: C2 +5.7 %, C4 +3.4 %.
-__device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best,
-                                               const Slopes* seg = nullptr) {
-#ifdef FS_MEAS_ROOT_ALL  // measurement builds only: every mesh root visited (frames differ)
-  return !zl || in_bounds(mn, mx, r.start);
-#endif
-#if FS_ROOT_BF
-  // The same decisions as below, as one straight-line mask computation: every
-  // certain outcome (the exact tests, and the magnitude tests away from their
-  // thresholds) folds into sure_miss, and only a lane that is neither certain
-  // nor a zero-length / both-ends-inside case branches to the reference's
-  // divisions. A slab parallel to the segment sends the lane there too (never
-  // seen on the bench scenes: |v_i| < 1e-5 over a whole segment).
+// is <= best). Exact by construction: slab times use the segment's v_rcp
+// slopes (relative error < 2.4e-7 against the reference's IEEE quotient of the
+// same difference), every sign test is exact, and a decision whose operands
+// lie within the error bound's margins of its threshold is redone with the
+// reference's divisions. The decisions are folded into straight-line masks
+// (sure_miss) with one branch to the exact path. The reference's test
+// fnear > ffar is max(n_i) > min(f_j); for i == j, n_i <= f_i holds exactly in
+// both (the same product sorted, or one product twice for a flat box), so only
+// a close cross-slab pair makes it unsure: a flat box (a wall, a quad light)
+// hit away from its edges stays certain. A slab parallel to the segment
+// (|v_i| < 1e-5, or a zero-length / tiny-substituted axis: a slope of
+// magnitude >= 1e5) takes the reference's path.
+// seg: the segment's slopes (seg_slopes); the reversed segment's are their
+// negation exactly (e - s = -(stop - start)).
+__device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool zl, float best, const Slopes& seg) {
   const bool si = in_bounds(mn, mx, r.start);
   const bool both = si && in_bounds(mn, mx, r.stop);
   const f3 s = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
-  bool par;
-  float rx, ry, rz;
-  if (FS_ROOT_HOIST && seg) {
-    // the segment's slopes, negated for the reversed segment (e - s = -(stop -
-    // start) exactly); |v_i| < 1e-5 (or a zero-length / tiny-substituted
-    // axis) shows as a slope of magnitude >= 1e5: the reference's path
-    par = fmaxf(fmaxf(fabsf(seg->ix), fabsf(seg->iy)), fabsf(seg->iz)) >= 99990.0f;
-    rx = si ? -seg->ix : seg->ix;
-    ry = si ? -seg->iy : seg->iy;
-    rz = si ? -seg->iz : seg->iz;
-  } else {
-    const f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
-    const f3 v = e - s;
-    par = cmp_eps(v.x, 0.0f, kEpsilon) || cmp_eps(v.y, 0.0f, kEpsilon) || cmp_eps(v.z, 0.0f, kEpsilon);
-    rx = __builtin_amdgcn_rcpf(v.x);
-    ry = __builtin_amdgcn_rcpf(v.y);
-    rz = __builtin_amdgcn_rcpf(v.z);
-  }
+  const bool par = fmaxf(fmaxf(fabsf(seg.ix), fabsf(seg.iy)), fabsf(seg.iz)) >= 99990.0f;
+  const float rx = si ? -seg.ix : seg.ix, ry = si ? -seg.iy : seg.iy, rz = si ? -seg.iz : seg.iz;
   const float ax = (mn.x - s.x) * rx, bx = (mx.x - s.x) * rx;
   const float ay = (mn.y - s.y) * ry, by = (mx.y - s.y) * ry;
   const float az = (mn.z - s.z) * rz, bz = (mx.z - s.z) * rz;
   const float n0 = fminf(ax, bx), f0 = fmaxf(ax, bx), n1 = fminf(ay, by), f1 = fmaxf(ay, by);
   const float n2 = fminf(az, bz), f2 = fmaxf(az, bz);
   const float fnear = fmaxf(fmaxf(n0, n1), n2), ffar = fminf(fminf(f0, f1), f2);
-#if FS_ROOT_TOL
-  // Margins from the error bound: a slab time here is (lo - s) * rcp(v), the
-  // reference's is the IEEE quotient of the same difference; v_rcp is within
+  // Margins from the error bound: a fast slab time is (lo - s) * rcp(v), the
+  // reference's the IEEE quotient of the same difference; v_rcp is within
   // 1 ulp, so the two differ by at most 2.4e-7 |t| (1 ulp + two roundings).
-  // fnear, ffar (min/max of such times) carry the same bound, 1 - fnear adds
-  // at most 6e-8 (exact for fnear in [0.5, 2]); the margins below are 4x that.
+  // fnear, ffar carry the same bound, 1 - fnear adds at most 6e-8 (exact for
+  // fnear in [0.5, 2]); the margins below are 4x that.
   auto close = [](float a, float b) { return fabsf(a - b) <= 1e-6f * (fabsf(a) + fabsf(b)); };
   const float tol2 = 1e-6f, tol3 = 1e-6f * fabsf(fnear) + 1e-7f;
-#else
-  auto close = [](float a, float b) { return fabsf(a - b) <= 1e-5f * (fabsf(a) + fabsf(b)); };
-  const float tol2 = 1e-5f, tol3 = 1e-5f;
-#endif
   bool u1 = close(fnear, ffar);
-  if (u1)  // a flat box hit away from its edges stays certain (FS_ROOT_PAIRS)
-    u1 = close(n0, f1) || close(n0, f2) || close(n1, f0) || close(n1, f2) || close(n2, f0) || close(n2, f1);
+  if (u1) u1 = close(n0, f1) || close(n0, f2) || close(n1, f0) || close(n1, f2) || close(n2, f0) || close(n2, f1);
   const bool u2 = fabsf(fnear - 1.0f) <= tol2;
   const float np = si ? 1.0f - fnear : fnear;
   const bool u3 = fabsf(np - best) <= tol3;
   const bool sure_miss = !par && ((ffar < 0) || (fnear < 0) || (!u1 && fnear > ffar) || (!u2 && fnear > 1.0f) ||
                                   (!u3 && np > best));
   bool visit = zl ? si : (both || !sure_miss);
-  FS_ROOT_STAT(0, true);
-  FS_ROOT_STAT(1, !zl && !both && !sure_miss && (par || u1 || u2 || u3));
-  FS_ROOT_STAT(2, !zl && !both && !sure_miss && par);
-  FS_ROOT_STAT(3, !zl && !both && !sure_miss && u1);
-  FS_ROOT_STAT(4, !zl && !both && !sure_miss && u2);
-  FS_ROOT_STAT(5, !zl && !both && !sure_miss && u3);
-  FS_ROOT_STAT(6, !zl && !both && !sure_miss && si);
-#ifndef FS_MEAS_NO_EXACT  // measurement builds only: no exact fallback (frames may differ)
   if (!zl && !both && !sure_miss && (par || u1 || u2 || u3)) {
-#if FS_ROOT_LITE
     // ray_intersect_bounds' worker (intersect.cpp:490-597) on the same
     // segment, straight-line: per slab the entry and exit times as the
     // reference's IEEE quotients ((lo - s) / v and (hi - s) / v, ordered by the
@@ -371,59 +263,8 @@ __device__ __forceinline__ bool ref_root_visit(f3 mn, f3 mx, const Ray& r, bool 
     }
     const float pe = si ? 1.0f - en : en;
     visit = hit && !(pe > best);
-#else
-    float pe;
-    visit = ref_ray_bounds(mn, mx, r, zl, pe) && !(pe > best);
-#endif
   }
-#endif
   return visit;
-#else
-  bool si = in_bounds(mn, mx, r.start);
-  if (zl) return si;                                 // param 0 (intersect.cpp:604-616)
-  if (si && in_bounds(mn, mx, r.stop)) return true;  // param 0 (:621-630)
-  f3 s = mk3(si ? r.stop.x : r.start.x, si ? r.stop.y : r.start.y, si ? r.stop.z : r.start.z);
-  f3 e = mk3(si ? r.start.x : r.stop.x, si ? r.start.y : r.stop.y, si ? r.start.z : r.stop.z);
-  f3 v = e - s;
-  bool outside = false;
-  float n[3], f[3];
-  auto slab = [&](int i, float sa, float va, float lo, float hi) {
-    if (cmp_eps(va, 0.0f, kEpsilon)) {
-      outside |= (sa < lo || sa > hi);
-      n[i] = -1e30f;
-      f[i] = 1e30f;
-      return;
-    }
-    float rc = __builtin_amdgcn_rcpf(va);
-    float t1 = (lo - sa) * rc, t2 = (hi - sa) * rc;
-    n[i] = fminf(t1, t2);
-    f[i] = fmaxf(t1, t2);
-  };
-  slab(0, s.x, v.x, mn.x, mx.x);
-  slab(1, s.y, v.y, mn.y, mx.y);
-  slab(2, s.z, v.z, mn.z, mx.z);
-  const float fnear = fmaxf(fmaxf(n[0], n[1]), fmaxf(n[2], -kInfinity));
-  const float ffar = fminf(fminf(f[0], f[1]), f[2]);
-  if (outside || ffar < 0 || fnear < 0) return false;  // exact tests
-  auto close = [](float a, float b) { return fabsf(a - b) <= 1e-5f * (fabsf(a) + fabsf(b)); };
-  bool unsure = close(fnear, ffar);
-#if FS_ROOT_PAIRS
-  if (unsure)
-    unsure = close(n[0], f[1]) || close(n[0], f[2]) || close(n[1], f[0]) || close(n[1], f[2]) ||
-             close(n[2], f[0]) || close(n[2], f[1]);
-#endif
-  if (!unsure && fnear > ffar) return false;
-  if (fabsf(fnear - 1.0f) <= 1e-5f)
-    unsure = true;
-  else if (fnear > 1) return false;
-  float np = si ? 1.0f - fnear : fnear;
-  if (fabsf(np - best) <= 1e-5f)
-    unsure = true;
-  else if (np > best) return false;
-  if (!unsure) return true;
-  float pe;
-  return ref_ray_bounds(mn, mx, r, zl, pe) && !(pe > best);
-#endif
 }
 
 // intersect.cpp:96-129 + 146-177: planar map, then barycentrics.
@@ -449,7 +290,6 @@ __device__ __forceinline__ void planar_bary(f4 pl, f3 v0, f3 v1, f3 vp, float& u
   v = (d00 * d12 - d01 * d02) * inv;
 }
 
-#if FS_TRI64
 // p1, v0, v1 hold the two components (a, b) the planar map keeps (fs_scene.h).
 struct TriData {
   float p1a, p1b, v0a, v0b, v1a, v1b;
@@ -508,46 +348,6 @@ __device__ __forceinline__ void bary_pre(const TriData& T, f3 pt, float& u, floa
   u = (T.d11 * d02 - T.d01 * d12) * T.inv;
   v = (T.d00 * d12 - T.d01 * d02) * T.inv;
 }
-#define FS_BARY_ARG(pt, T) (pt)
-#else
-struct TriData {
-  f3 p1, v0, v1;
-  float d00, d01, d11, inv;
-  uint32_t axis, face;
-  f4 pl;
-  bool same_plane;
-};
-__device__ __forceinline__ TriData load_tri(const DevTri* __restrict__ T, uint32_t i) {
-  const float4* q = reinterpret_cast<const float4*>(T + i);
-  float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
-  TriData t;
-  t.p1 = mk3(a.x, a.y, a.z);
-  t.face = __float_as_uint(a.w);
-  t.v0 = mk3(b.x, b.y, b.z);
-  t.d00 = b.w;
-  t.v1 = mk3(c.x, c.y, c.z);
-  t.d01 = c.w;
-  t.d11 = d.x;
-  t.inv = d.y;
-  t.axis = __float_as_uint(d.z);
-  t.pl = mk4(e.x, e.y, e.z, e.w);
-  t.same_plane = (__float_as_uint(d.w) & kSamePlaneBit) != 0;
-  return t;
-}
-__device__ __forceinline__ TriData load_tri_uniform(const DevTri* T, uint32_t i) { return load_tri(T, i); }
-__device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint32_t i) { return T[i].face; }
-// intersect.cpp:146-177 with the triangle-only terms precomputed: vp is
-// planar-mapped like v0/v1 and the reference's dot products follow.
-__device__ __forceinline__ void bary_pre(const TriData& T, f3 vp, float& u, float& v) {
-  if (T.axis == 0) vp.x = 0;
-  if (T.axis == 1) vp.y = 0;
-  if (T.axis == 2) vp.z = 0;
-  float d02 = dot(T.v0, vp), d12 = dot(T.v1, vp);
-  u = (T.d11 * d02 - T.d01 * d12) * T.inv;
-  v = (T.d00 * d12 - T.d01 * d02) * T.inv;
-}
-#define FS_BARY_ARG(pt, T) ((pt) - (T).p1)
-#endif
 
 // intersect.cpp:357-419 (non-zero-length branch)
 __device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t, f3& p, float& u, float& v) {
@@ -555,7 +355,7 @@ __device__ __forceinline__ bool ray_tri(const TriData& T, const Ray& r, float& t
   f3 pp;
   if (!ray_plane(T.pl, r, tt, pp)) return false;
   float uu, vv;
-  bary_pre(T, FS_BARY_ARG(pp, T), uu, vv);
+  bary_pre(T, pp, uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     t = tt;
     p = pp;
@@ -571,7 +371,7 @@ __device__ __forceinline__ bool point_in_tri(const TriData& T, f3 pt, float& u, 
   float d4 = T.pl.x * pt.x + T.pl.y * pt.y + T.pl.z * pt.z + T.pl.w * 1.0f;
   if (!cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) return false;
   float uu, vv;
-  bary_pre(T, FS_BARY_ARG(pt, T), uu, vv);
+  bary_pre(T, pt, uu, vv);
   if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
     u = uu;
     v = vv;
@@ -920,9 +720,9 @@ __device__ __forceinline__ ConstObj const_obj(const DevObject* base, uint32_t i)
 
 // The first 64 B of an object record (kind, material, i0-i5, d0-d7): what the
 // object loop reads for meshes, spheres, planes and discs, fetched as one
-// scalar load at the top of the object's iteration (FS_OBJ_HEAD) instead of
-// field by field where each is first used (three or four dependent scalar
-// round trips per object).
+// scalar load at the top of the object's iteration instead of field by field
+// where each is first used (three or four dependent scalar round trips per
+// object: C4 +1.4 %).
 struct ObjHead {
   int32_t kind, mat, i0, i1, i2, i3, i4, i5;
   float d[8];
@@ -1037,7 +837,7 @@ __device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t fir
     }
     if (on_plane) {
       float uu, vv;
-      bary_pre(T, FS_BARY_ARG(pp, T), uu, vv);
+      bary_pre(T, pp, uu, vv);
       if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
         bool better = tt < h.t || (tt == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
         if (better) {
@@ -1074,9 +874,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   }
   float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;  // h.t only changes in the leaf tests
   bool susp = false;
-#if FS_TRAV_PRIO
-  __builtin_amdgcn_s_setprio(FS_TRAV_PRIO);
-#endif
   while ((w != kNone || leaf) && !(SUSP && susp)) {
     while (!(w & kLeafBit) && w != kNone) {
       const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
@@ -1096,17 +893,15 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
         float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
         float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
-        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
-#if FS_SLAB_IMIN
+        // The exit clamp to the walk's t limit is a signed-integer min on the
+        // float bits: the limit is positive, so for finite exits the integer
+        // order is the float order, and v_min_f32 would need the loop-carried
+        // limit re-canonicalised on every trip (C4 +1 %).
         const int tl = __float_as_int(tmax_lim);
+        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
         float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), __int_as_float(min(__float_as_int(fmaxf(g0, k0)), tl)));
         float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
         float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), __int_as_float(min(__float_as_int(fmaxf(g1, k1)), tl)));
-#else
-        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), fminf(fmaxf(g0, k0), tmax_lim));
-        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
-        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), fminf(fmaxf(g1, k1), tmax_lim));
-#endif
         h0 = n0 <= f0;
         h1 = n1 <= f1;
         t0 = n0;
@@ -1139,7 +934,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       }
     }
     if (SUSP && susp) break;
-#if FS_FLAT_LEAF
     // One triangle per lane per trip, running on through the leaves the walk
     // stopped on (the popped far children may be leaves too), so a lane with
     // 1+2 triangles costs the wave 3 trips, not max-per-leaf 2+2.
@@ -1162,25 +956,8 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         leaf = 0;
       }
     }
-#else
-    while (leaf) {
-#ifdef FS_PHASE_PROF
-      FS_WAVE_TRIP(tally.leaf_trips);
-      tally.lane_leaves++;
-#endif
-      test_leaf<COUNT, ZLMODE>(S, leaf, oi, r, zl, h, tally);
-      leaf = 0;
-      if (w & kLeafBit) {  // the walk also stopped on a leaf: test it next
-        leaf = w;
-        w = sp ? stk[--sp * kBlock] : kNone;
-      }
-    }
-#endif
     tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
   }
-#if FS_TRAV_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   if (SUSP && susp) {
     ws->oi = oi;
     ws->w = w;
@@ -1188,193 +965,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
     ws->sp = sp;
   }
   return SUSP && susp;
-}
-
-// ---- the walk pool (POOL schedule) -----------------------------------------
-// A workgroup of kPoolWaves waves: wave 0 walks BVHs for the others, which
-// run everything else (tasks, the object loop, shading, the backward pass).
-// A lane that reaches a mesh with a BVH writes its segment into its own slot
-// of the workgroup's LDS pool and waits; the walk wave keeps its 64 lanes
-// busy with the pending walks of all three waves (refilling lanes as walks
-// finish), and posts each result back into the slot. The walk's operations
-// are those of traverse_ww, only on another lane: frames are identical.
-// Measured: the node loop ran 27 % of its lanes per trip in
-// the walking wave itself, and the kernel is VALU-issue bound.
-constexpr uint32_t kPoolWaves = 4;                       // 1 walk wave + 3 shading waves
-constexpr uint32_t kPoolSlots = (kPoolWaves - 1) * kBlock;
-constexpr uint32_t kPoolNoSlot = 0xFFFFFFFFu;
-constexpr uint32_t kPoolZl = 0x80000000u;                // root word bit: zero-length segment
-struct WalkPool {
-  // per slot (SoA): segment start, dir, the best t so far, root node | kPoolZl;
-  // after the walk the same words hold the result: t, u, v, prim (kPoolNoSlot: none), point
-  float f[8][kPoolSlots];
-  unsigned long long pending[kPoolWaves - 1];  // slots waiting for a walk (set by shaders, cleared by the walker)
-  unsigned long long done[kPoolWaves - 1];     // results posted (set by the walker, cleared by shaders)
-  uint32_t alive;                              // shading waves still running
-};
-
-__device__ __forceinline__ unsigned long long lds_load64(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// position of the n-th (0-based) set bit of m (n < popcount(m))
-__device__ __forceinline__ uint32_t nth_set_bit(unsigned long long m, uint32_t n) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t half = 32; half; half >>= 1) {
-    const uint32_t c = (uint32_t)__popcll(m & ((1ull << half) - 1ull));
-    if (n >= c) {
-      n -= c;
-      m >>= half;
-      pos += half;
-    }
-  }
-  return pos;
-}
-
-// The walk wave. Lanes hold one pool slot's walk each; after every pass
-// (inner nodes until each lane holds a leaf, or until at most `refill`
-// lanes still walk while slots are pending; then the parked leaves) finished
-// lanes post their results and free lanes take pending slots, oldest wave
-// first in turn. Exits once every shading wave has exited (their waits all
-// ended) and no slot is pending.
-template <bool COUNT>
-__device__ void walk_service(const DevScene& S, WalkPool& pool, uint32_t* __restrict__ stk, uint32_t refill,
-                             Tally<COUNT>& tally) {
-  constexpr uint32_t kNone = 0x7FFFFFFFu;
-  const uint32_t lane = threadIdx.x & (kBlock - 1);
-  uint32_t slot = kPoolNoSlot;
-  uint32_t w = kNone, leaf = 0, sp = 0;
-  float tmax_lim = 0.0f;
-  bool zl = false;
-  Ray r;
-  Slopes sl{};
-  MinHit h;
-  h.t = 2.0f;
-  h.obj = -1;
-  uint32_t turn = 0;
-  for (;;) {
-    // 1. post finished walks
-    const bool fin = slot != kPoolNoSlot && w == kNone && leaf == 0;
-    if (fin) {
-      pool.f[0][slot] = h.t;
-      pool.f[1][slot] = h.u;
-      pool.f[2][slot] = h.v;
-      pool.f[3][slot] = __uint_as_float(h.obj >= 0 ? h.prim : kPoolNoSlot);
-      pool.f[4][slot] = __uint_as_float(h.point);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __hip_atomic_fetch_or(&pool.done[slot >> 6], 1ull << (slot & 63), __ATOMIC_RELEASE,
-                            __HIP_MEMORY_SCOPE_WORKGROUP);
-      slot = kPoolNoSlot;
-    }
-    // 2. free lanes take pending slots
-    const unsigned long long freem = __ballot(slot == kPoolNoSlot);
-    uint32_t nfree = (uint32_t)__popcll(freem);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(freem >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)freem, 0u));
-    uint32_t base = 0;
-    bool any_pending = false;
-    for (uint32_t k = 0; k < kPoolWaves - 1; k++) {
-      const uint32_t sw = __builtin_amdgcn_readfirstlane((turn + k) % (kPoolWaves - 1));
-      unsigned long long pm = lds_load64(&pool.pending[sw]);
-      pm = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(pm >> 32)) << 32) |
-           (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pm);
-      if (!pm) continue;
-      if (!nfree) {
-        any_pending = true;
-        continue;
-      }
-      unsigned long long take = pm;
-      if ((uint32_t)__popcll(pm) > nfree) {  // the lowest nfree pending slots
-        const uint32_t cut = __builtin_amdgcn_readfirstlane(nth_set_bit(pm, nfree));
-        take = pm & ((1ull << cut) - 1ull);
-        any_pending = true;
-      }
-      const uint32_t nt = (uint32_t)__popcll(take);
-      if (lane == (uint32_t)__builtin_amdgcn_readfirstlane(lane))
-        __hip_atomic_fetch_and(&pool.pending[sw], ~take, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (slot == kPoolNoSlot && rank >= base && rank < base + nt) slot = sw * kBlock + nth_set_bit(take, rank - base);
-      base += nt;
-      nfree -= nt;
-    }
-    turn++;
-    const bool fresh = slot != kPoolNoSlot && (freem >> lane & 1ull);
-    if (fresh) {  // the new walk: segment, best t, root (traverse_ww's start)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      r.start = mk3(pool.f[0][slot], pool.f[1][slot], pool.f[2][slot]);
-      r.dir = mk3(pool.f[3][slot], pool.f[4][slot], pool.f[5][slot]);
-      h.t = pool.f[6][slot];
-      const uint32_t rw = __float_as_uint(pool.f[7][slot]);
-      zl = (rw & kPoolZl) != 0;
-      w = rw & ~kPoolZl;
-      leaf = 0;
-      sp = 0;
-      h.obj = -1;
-      h.prim = 0;
-      h.u = h.v = 0.0f;
-      h.point = 0;
-      sl = walk_slopes(r, zl);
-      tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
-    }
-    if (!__ballot(slot != kPoolNoSlot)) {
-      if (__hip_atomic_load(&pool.alive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    // 3. one pass: inner nodes (while-while, postponed leaves), then the leaves
-    const uint32_t thr = any_pending ? refill : 0u;
-    {
-      const float ix = sl.ix, iy = sl.iy, iz = sl.iz, ox = sl.ox, oy = sl.oy, oz = sl.oz;
-      while (!(w & kLeafBit) && w != kNone) {
-        const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
-        float4 X = q[0], Y = q[1], Z = q[2];
-        uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
-        if (COUNT) tally.nodes++;
-        float a0 = fmaf(X.x, ix, ox), b0 = fmaf(X.z, ix, ox);
-        float a1 = fmaf(X.y, ix, ox), b1 = fmaf(X.w, ix, ox);
-        float c0 = fmaf(Y.x, iy, oy), e0 = fmaf(Y.z, iy, oy);
-        float c1 = fmaf(Y.y, iy, oy), e1 = fmaf(Y.w, iy, oy);
-        float g0 = fmaf(Z.x, iz, oz), k0 = fmaf(Z.z, iz, oz);
-        float g1 = fmaf(Z.y, iz, oz), k1 = fmaf(Z.w, iz, oz);
-        const int tl = __float_as_int(tmax_lim);
-        float n0 = fmaxf(fmaxf(fminf(a0, b0), fminf(c0, e0)), fmaxf(fminf(g0, k0), -1e-6f));
-        float f0 = fminf(fminf(fmaxf(a0, b0), fmaxf(c0, e0)), __int_as_float(min(__float_as_int(fmaxf(g0, k0)), tl)));
-        float n1 = fmaxf(fmaxf(fminf(a1, b1), fminf(c1, e1)), fmaxf(fminf(g1, k1), -1e-6f));
-        float f1 = fminf(fminf(fmaxf(a1, b1), fmaxf(c1, e1)), __int_as_float(min(__float_as_int(fmaxf(g1, k1)), tl)));
-        const bool h0 = n0 <= f0, h1 = n1 <= f1;
-        if (h0 && h1) {
-          const bool swap = n1 < n0;
-          stk[sp * kBlock] = swap ? Cw.x : Cw.y;
-          sp++;
-          w = swap ? Cw.y : Cw.x;
-        } else if (h0 || h1) {
-          w = h0 ? Cw.x : Cw.y;
-        } else {
-          w = sp ? stk[--sp * kBlock] : kNone;
-        }
-        if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
-          leaf = w;
-          w = sp ? stk[--sp * kBlock] : kNone;
-        }
-        if (__ballot(leaf == 0) == 0) break;  // every lane in the loop holds a leaf
-        if ((uint32_t)__popcll(__builtin_amdgcn_read_exec()) <= thr) break;  // few walk: refill first
-      }
-      while (leaf) {  // one triangle per lane per trip (FS_FLAT_LEAF)
-        uint32_t cnt = leaf_count(leaf);
-        if (cnt) {
-          test_leaf<COUNT>(S, leaf_word(1, leaf & kLeafFirstMask), 1, r, zl, h, tally);
-          cnt--;
-        }
-        if (cnt) {
-          leaf = leaf_word(cnt, (leaf & kLeafFirstMask) + 1u);
-        } else if (w & kLeafBit) {
-          leaf = w;
-          w = sp ? stk[--sp * kBlock] : kNone;
-        } else {
-          leaf = 0;
-        }
-      }
-      tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;
-    }
-  }
 }
 
 // Conservative segment-vs-box cull for analytic objects (not a reference
@@ -1420,7 +1010,7 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
   // bench.py's byte model weighs object_loads per wave
   if (COUNT) tally.lane_objs++;
   if (kind == FS_OBJ_MESH) {
-    if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t)) return false;
+    if (!o->i2 || !ref_root_visit(mk3(d[0], d[1], d[2]), mk3(d[3], d[4], d[5]), r, zl, h.t, *slp)) return false;
     const int32_t before = h.obj;
     if (o->i3)
       small_mesh_trace<COUNT>(S, __float_as_uint(d[6]), (uint32_t)o->i3, (int32_t)oi, r, zl, h, tally);
@@ -1523,7 +1113,7 @@ __device__ void scene_trace_tree(const DevScene& S, const Ray& r, MinHit& h, uin
   h.point = 0;
   h.tc = -1;
   const bool zl = zero_len(r);
-  const Slopes sl = walk_slopes(r, zl);
+  const Slopes sl = seg_slopes(r, zl);  // the mesh-root culls' and the walks' (as the object list's)
   const DevSceneTree& T = *S.tree;
   const f3 rmn = mk3(T.root_mn[0], T.root_mn[1], T.root_mn[2]), rmx = mk3(T.root_mx[0], T.root_mx[1], T.root_mx[2]);
   const f3 ctr = mk3(T.center[0], T.center[1], T.center[2]);
@@ -1587,23 +1177,20 @@ __device__ void scene_trace_tree(const DevScene& S, const Ray& r, MinHit& h, uin
   }
 }
 
+// Scene::Trace's object loop (scene.cpp:227-236) into the lean hit record.
 // SUSP: a lane may park inside a mesh walk (*parked = true, state in *ws) and
 // resume it in a later call with the same ray: objects before the parked one
 // are skipped on resume (already processed), the rest follow in order.
-template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false, bool NOWALK = false,
-          bool POOL = false>
+template <bool COUNT, bool TEX = false, bool SUSP = false, bool SOCT = false, bool NOWALK = false>
 __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r, MinHit& h,
                                                 uint32_t* __restrict__ stk, Tally<COUNT>& tally,
                                                 PhaseAcc& pa, WalkSuspend* ws = nullptr, uint32_t susp_thr = 0,
-                                                uint32_t susp_thr_small = 0,
-                                                bool* parked = nullptr, WalkPool* pool = nullptr,
-                                                uint32_t sw = 0) {
-  constexpr bool PARK = SUSP || POOL;  // a lane may leave the object loop mid-way and come back
+                                                uint32_t susp_thr_small = 0, bool* parked = nullptr) {
   if (SOCT) {  // Scene::Trace with a valid object tree (scene.cpp:231-236)
     scene_trace_tree<COUNT, TEX>(S, r, h, stk, tally);
     return;
   }
-  bool resuming = PARK && ws->oi >= 0;
+  bool resuming = SUSP && ws->oi >= 0;
   if (!resuming) {
     h.t = 2.0f;
     h.obj = -1;
@@ -1614,34 +1201,23 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   }
   bool zl = zero_len(r);
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
-  const uint32_t me = sw * kBlock + (threadIdx.x & (kBlock - 1));  // POOL: this lane's slot
   bool park = false;
-#if FS_HOIST_SLOPES
-  const Slopes sl = FS_ROOT_HOIST ? seg_slopes(r, zl) : walk_slopes(r, zl);  // once per segment
-  const Slopes* slp = &sl;
-#else
-  const Slopes* slp = nullptr;
-#endif
+  const Slopes sl = seg_slopes(r, zl);  // once per segment: the mesh-root culls' and the walks'
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
-    if (PARK && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
+    if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
-#if FS_OBJ_HEAD
     const ObjHead H = load_head(o);
     const float* hd = H.d;
-#else
-    const auto& H = *o;
-    const __attribute__((address_space(4))) float* hd = o->d;
-#endif
     const int32_t kind = H.kind;
     const __attribute__((address_space(4))) float* d = o->d;
     if (kind == FS_OBJ_MESH) {
       if (!H.i2) continue;
       uint64_t t0 = FS_TICK();
-      const bool resume_here = PARK && resuming && (uint32_t)ws->oi == oi;
+      const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
       bool visit =
-          resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t, slp);
+          resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t, sl);
       uint64_t t1 = FS_TICK();
       if (H.i3) {  // a small mesh: its faces, no walk (never parks)
         if (visit)
@@ -1652,52 +1228,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
       } else if (NOWALK) {
         // every mesh of the scene is small (chosen at upload): no BVH walk
-      } else if (POOL) {
-        // the walk goes to the pool: the segment, the best t so far and the
-        // root into this lane's slot; the lane leaves the object loop and
-        // comes back here with the walk's result (kernel: the done bit)
-        const bool submit = visit && !resume_here;
-        if (submit) {
-          pool->f[0][me] = r.start.x;
-          pool->f[1][me] = r.start.y;
-          pool->f[2][me] = r.start.z;
-          pool->f[3][me] = r.dir.x;
-          pool->f[4][me] = r.dir.y;
-          pool->f[5][me] = r.dir.z;
-          pool->f[6][me] = h.t;
-          pool->f[7][me] = __uint_as_float((uint32_t)H.i0 | (zl ? kPoolZl : 0u));
-        }
-        const unsigned long long sm = __ballot(submit);
-        if (sm && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __hip_atomic_fetch_or(&pool->pending[sw], sm, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (submit) {
-          ws->oi = (int32_t)oi;
-          park = true;
-          continue;
-        }
-        if (resume_here) {  // the walk of MeshBvhNode::Trace, posted by the walk wave
-          const uint32_t prim = __float_as_uint(pool->f[3][me]);
-          if (prim != kPoolNoSlot) {
-            h.t = pool->f[0][me];
-            h.obj = (int32_t)oi;
-            h.prim = prim;
-            h.u = pool->f[1][me];
-            h.v = pool->f[2][me];
-            h.point = __float_as_uint(pool->f[4][me]);
-          }
-          resuming = false;
-        }
       } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
-        // (deferring a walk's start until enough lanes want it, parked at the
-        // root: C4 -1 to -10 %, C3 -11 to +1.6 %, and its code alone cost C3
-        // 1.3 %: removed)
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
-                                          H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u), live, slp);
+                                          H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u), live, &sl);
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
         if (park) {
@@ -1707,7 +1243,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
 #endif
         if (park) continue;
       } else if (visit) {
-        traverse_ww<COUNT>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, slp);
+        traverse_ww<COUNT>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, nullptr, false, 0u, 0u, &sl);
       }
       // MeshObject::Trace writes surface_texcoords only when the mesh has
       // texcoords (mesh.cpp:300-311); otherwise the previous writer's stay.
@@ -1780,7 +1316,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     pa.prim += FS_TICK() - tp0;
 #endif
   }
-  if (PARK) {
+  if (SUSP) {
     if (!park) ws->oi = -1;
     *parked = park;
   }
@@ -1897,7 +1433,7 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
   p = h.point ? r.start : r.start + r.dir * h.t;
   int32_t kind = o->kind;
   if (kind == FS_OBJ_MESH) {
-    const float4 pl = reinterpret_cast<const float4*>(S.tris + h.prim)[FS_TRI64 ? 0 : 4];  // face plane
+    const float4 pl = reinterpret_cast<const float4*>(S.tris + h.prim)[0];  // face plane
     n = mk3(pl.x, pl.y, pl.z);
     if (o->i1) {
       const float4* nq = S.tri_normals + 3 * (size_t)h.prim;
@@ -2046,7 +1582,7 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 
 // The path-trace megakernel: path regeneration with a lean register
 // footprint. The closest-hit query keeps only (t, object, primitive, u, v);
-// the per-bounce shading scalars and the Fog anchors live in per-lane HBM
+// the per-bounce shading scalars and the Fog anchors live in per-lane
 // scratch rows of the wave; the depth-0 AOVs go straight to the frame.
 //
 // Work: the wave's lanes share one pool of (pixel, sample) tasks. Whenever
@@ -2058,62 +1594,39 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 // pull blocks until every queue is empty: the launch tail is one task
 // path, not one block. Each sample's radiance goes to its block's radiance
 // row; fold_groups folds the rows into the frame in sample order.
+//
+// NOWALK (every mesh small): no walk stack; the per-bounce shading scalars
+// (c and Ceramic's term, [level][lane]) are staged in LDS instead of HBM
+// scratch rows, so the backward pass reads them at LDS latency and the L2
+// no longer holds (and writes back) the rows. SUSP (the parked-walk kernel):
+// the HBM rows are lane-major ([lane][level]), so the backward pass loads a
+// path's eight c values in two 16-B loads (C4 +3.5 %).
 template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false,
-          bool NOWALK = false, bool POOL = false>
-__global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
-                                                                     float2* __restrict__ lvl_all,
-                                                                     float4* __restrict__ anchor_all,
-                                                                     float4* __restrict__ tex_all,
-                                                                     float* __restrict__ rad_all,
-                                                                     uint32_t* __restrict__ mat_all,
-                                                                     uint32_t* __restrict__ queues,
-                                                                     DevCounters* __restrict__ counters) {
-  // NOWALK (every mesh small): no walk stack; the per-bounce shading scalars
-  // (c and Ceramic's term, [level][lane]) are staged in LDS instead of HBM
-  // scratch rows, so the backward pass reads them at LDS latency and the L2
-  // no longer holds (and writes back) the rows.
-  // POOL: the shading waves' rows in LDS too (the walk stack and the pool
-  // take 12 KiB of a 4-wave workgroup's 26 KiB share at 6 waves per SIMD).
-  constexpr bool kLdsRows = NOWALK || (POOL && FS_POOL_LDS_ROWS);
-  constexpr bool kLaneRows = FS_ROWS_LANE && !kLdsRows && SUSP;  // HBM rows lane-major (unwind's LROWS)
+          bool NOWALK = false>
+__global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
+                                                                    float2* __restrict__ lvl_all,
+                                                                    float4* __restrict__ anchor_all,
+                                                                    float4* __restrict__ tex_all,
+                                                                    float* __restrict__ rad_all,
+                                                                    uint32_t* __restrict__ mat_all,
+                                                                    uint32_t* __restrict__ queues,
+                                                                    DevCounters* __restrict__ counters) {
+  constexpr bool kLdsRows = NOWALK;
+  constexpr bool kLaneRows = !kLdsRows && SUSP;  // HBM rows lane-major (unwind's LROWS)
   __shared__ uint32_t stk_all[NOWALK ? 1 : kTraversalStack * kBlock];
-  __shared__ float2 lvl_lds[kLdsRows ? (POOL ? kPoolWaves - 1 : 1) * kMaxDepth * kBlock : 1];
-  // POOL: workgroups of kPoolWaves waves; wave 0 walks for the others (walk_service)
-  const uint32_t wave = POOL ? threadIdx.x / kBlock : 0u;
+  __shared__ float2 lvl_lds[kLdsRows ? kMaxDepth * kBlock : 1];
   const uint32_t lane = threadIdx.x % kBlock;
-  const uint32_t wid = POOL ? blockIdx.x * (kPoolWaves - 1) + wave - 1u : blockIdx.x;  // this shading wave's rows
-  WalkPool* pool = nullptr;
+  const uint32_t wid = blockIdx.x;  // this wave's rows
   Tally<COUNT> tally;
-  if constexpr (POOL) {
-    __shared__ WalkPool pool_lds;
-    pool = &pool_lds;
-    if (threadIdx.x < kPoolWaves - 1) {
-      pool->pending[threadIdx.x] = 0;
-      pool->done[threadIdx.x] = 0;
-    }
-    if (threadIdx.x == 0) pool->alive = kPoolWaves - 1;
-    __syncthreads();
-    if (wave == 0) {
-      walk_service<COUNT>(S, *pool, stk_all + lane, P.pool_refill, tally);
-      if (COUNT) {
-        atomicAdd(&counters->node_visits, (unsigned long long)tally.nodes);
-        atomicAdd(&counters->tri_tests, (unsigned long long)tally.tris);
-      }
-      return;
-    }
-  }
   uint32_t* stk = stk_all + lane;
-  // Scratch rows of the wave, depth-major ([level][lane]) so a wave's store
-  // is one contiguous run; addressed as wave base (SGPR) + 32-bit lane offset.
-  float2* lvl = kLdsRows ? lvl_lds + (POOL ? (wave - 1) * (kMaxDepth * kBlock) : 0u)
-                         : lvl_all + (size_t)wid * (kMaxDepth * kBlock);
+  // Scratch rows of the wave, addressed as wave base (SGPR) + 32-bit lane offset.
+  float2* lvl = kLdsRows ? lvl_lds : lvl_all + (size_t)wid * (kMaxDepth * kBlock);
   float4* anchor = anchor_all + (size_t)wid * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
   float4* texrow = tex_all + (size_t)wid * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   TaskBlock cur;  // the block the wave hands out tasks from
   uint32_t queue = blockIdx.x & 7u, queues_left = P.persist ? 8u : 1u;
-  uint32_t idle = 0;  // POOL: iterations in a row in which every lane waited (watchdog)
   uint32_t segments = 0, samples_done = 0;
 
   // the lane's task: its pixel, sample and radiance slot
@@ -2206,7 +1719,6 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
     FS_PHASE(1);
     const bool aov = (slot >> 31) != 0;
     bool done = false;
-    bool waited = false;  // POOL: the lane only waited for its walk this iteration
     f3 L = mk3(0, 0, 0);
     if (depth >= kMaxDepth) {
       done = true;
@@ -2214,104 +1726,21 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
       L = mk3(1, 1, 1);
       done = true;
     } else {
-      if (!(SUSP || POOL) || ws.oi < 0) segments++;
+      if (!SUSP || ws.oi < 0) segments++;
       bool parked = false;
-#ifdef FS_PHASE_PROF
       PhaseAcc pa;
-#ifdef FS_PHASE_HIST
-      const uint32_t nodes_before = tally.lane_nodes, leaves_before = tally.lane_leaves;
-#endif
       scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
-                                                        &parked);
+                                                      &parked);
+#ifdef FS_PHASE_PROF
       ph[5] += pa.cull;
       ph[6] += pa.trav;
       ph[7] += pa.prim;
       ph[10] += pa.small;
-      FS_PHASE(2);
-#ifdef FS_PHASE_HIST
-      {  // histogram of node visits per traced segment: 0,1-4,5-8,9-16,17-32,33-64,65-128,>128
-        uint32_t nv = tally.lane_nodes - nodes_before, bin = 0;
-        if (nv > 0) bin = 1;
-        if (nv > 4) bin = 2;
-        if (nv > 8) bin = 3;
-        if (nv > 16) bin = 4;
-        if (nv > 32) bin = 5;
-        if (nv > 64) bin = 6;
-        if (nv > 128) bin = 7;
-        atomicAdd(&counters->phase[16 + bin], 1ull);
-        // bound for per-lane object sequencing: the wave's max over lanes of
-        // this call's node visits / leaf tests (vs node/leaf wave trips)
-        __shared__ uint32_t red[2];
-        const uint32_t nl = tally.lane_leaves - leaves_before;
-        const bool first = threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x);
-        if (first) red[0] = red[1] = 0;
-        atomicMax(&red[0], nv);
-        atomicMax(&red[1], nl);
-        if (first) {
-          atomicAdd(&counters->phase[24], (unsigned long long)red[0]);
-          atomicAdd(&counters->phase[25], (unsigned long long)red[1]);
-        }
-      }
-#endif
-      tk = __builtin_readcyclecounter();  // the histogram's own time is left out
-#endif
-#ifdef FS_PHASE_PROF
       act[0] += (uint64_t)__popcll(__ballot(1));
       act[1] += (uint64_t)__popcll(__ballot(!(SUSP && parked) && h.obj >= 0));
-#else
-      PhaseAcc pa;
-      if constexpr (POOL) {
-        // a lane waiting for its walk goes on once the walk wave posted it
-        const unsigned long long dm = lds_load64(&pool->done[wave - 1]);
-        const bool ready = ws.oi >= 0 && ((dm >> lane) & 1ull);
-        parked = ws.oi >= 0 && !ready;
-        // Clear the done bits first: a resumed lane reads its result in the
-        // trace below and may post its next walk into the same slot there,
-        // whose done bit the walk wave can set before this wave goes on.
-        const unsigned long long cm = __ballot(ready);
-        if (cm && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
-          __hip_atomic_fetch_and(&pool->done[wave - 1], ~cm, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (!parked)
-          scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK, POOL>(S, r, h, stk, tally, pa, &ws, P.susp_thr,
-                                                                P.susp_thr_small, &parked, pool, wave - 1);
-        if (P.pool_sync) {
-          // Wait (sleeping: the SIMD issues the other waves) for the walks this
-          // wave just posted and finish those lanes' object loops in the same
-          // iteration, so every lane shades its segment together.
-          for (uint32_t round = 0;; round++) {
-            const unsigned long long pm = __ballot(parked);
-            if (!pm) break;
-            uint32_t spins = 0;
-            while ((lds_load64(&pool->done[wave - 1]) & pm) != pm && spins < (1u << 24)) {
-              __builtin_amdgcn_s_sleep(1);
-              spins++;
-            }
-            if (spins >= (1u << 24) || round > 64) {  // a stalled pool: end with a bad frame, not a hang
-              if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) atomicOr(P.status, 1u);
-              if (parked) {
-                ws.oi = -1;
-                h.obj = -1;
-                parked = false;
-              }
-              break;
-            }
-            if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
-              __hip_atomic_fetch_and(&pool->done[wave - 1], ~pm, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (parked) {
-              parked = false;
-              scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK, POOL>(S, r, h, stk, tally, pa, &ws, P.susp_thr,
-                                                                    P.susp_thr_small, &parked, pool, wave - 1);
-            }
-          }
-        }
-        waited = parked;
-      } else {
-        scene_trace_min<COUNT, TEX, SUSP, SOCT, NOWALK>(S, r, h, stk, tally, pa, &ws, P.susp_thr, P.susp_thr_small,
-                                                        &parked);
-      }
 #endif
       FS_PHASE(2);
-      if ((SUSP || POOL) && parked) {
+      if (SUSP && parked) {
         // the walk is parked; the lane resumes it next iteration
       } else if (h.obj < 0) {
         if (depth == 1 && (slot & kFog0)) *at_byte(anchor, a1_off) = make_float4(r.stop.x, r.stop.y, r.stop.z, 0);
@@ -2352,11 +1781,9 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
-#ifndef FS_MEAS_NO_LVL  // measurement builds only (tools/gpu_writes.sh): the write streams one by one
         *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, false) * 4u) = c;
         if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)
           *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, true) * 4u) = ds;
-#endif
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0 && kind == FS_MAT_FOG) {  // Fog draws with the distance of its two anchors
@@ -2398,24 +1825,12 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
         p0 = mk3(a.x, a.y, a.z);
         lp0 = mk3(b.x, b.y, b.z);
       }
-#ifndef FS_MEAS_NO_UNWIND  // measurement builds only: no backward pass (frames differ)
       L = unwind<TEX, MMAT, !SUSP, kLaneRows>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
-#else
-      L.x += (float)top + p0.x + lp0.x;
-#endif
+      // [sample][pixel][channel]: one 12-B record per sample (the planar
+      // [channel][sample][pixel] rows wrote 50 B per sample back from L2)
       float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);
       const uint32_t o = slot & ~(0x80000000u | kFog0);
-#ifndef FS_MEAS_NO_RAD
-#if FS_RAD_XYZ  // [sample][pixel][channel]: one 12-B store per sample
       store_rgb(rad + 3 * o, L);
-#else  // [channel][sample][pixel]
-      rad[o] = L.x;
-      rad[P.spp * kBlock + o] = L.y;
-      rad[2 * P.spp * kBlock + o] = L.z;
-#endif
-#else
-      if (L.x == 1234.5f) rad[o] = L.y;  // keeps L live
-#endif
       if (COUNT) samples_done++;
       fresh = true;
     }
@@ -2423,21 +1838,6 @@ __global__ __launch_bounds__(POOL ? kPoolWaves * kBlock : kBlock, WAVES) void re
 #ifdef FS_PHASE_PROF
     ph[8]++;
 #endif
-    if constexpr (POOL) {  // every lane waits: let the walk wave run (and a watchdog for a stalled pool)
-      if (__ballot(!waited)) {
-        idle = 0;
-      } else {
-        __builtin_amdgcn_s_sleep(1);
-        if (++idle > (1u << 24)) {
-          if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) atomicOr(P.status, 1u);
-          break;
-        }
-      }
-    }
-  }
-  if constexpr (POOL) {  // this shading wave is done: the walk wave exits after the last one
-    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x))
-      __hip_atomic_fetch_sub(&pool->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 #ifdef FS_PHASE_PROF
   ph[9] = __builtin_readcyclecounter() - t_begin;
@@ -2486,11 +1886,7 @@ __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, cons
     const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * P.spp * kBlock);
     for (uint32_t k = 0; k < P.spp; k++) {
       const uint32_t o = k * kBlock + lane;
-#if FS_RAD_XYZ
       f3 L = mk3(rad[3 * o], rad[3 * o + 1], rad[3 * o + 2]);
-#else
-      f3 L = mk3(rad[o], rad[P.spp * kBlock + o], rad[2 * P.spp * kBlock + o]);
-#endif
       f3 np = mean * (float)n + L;
       float dv = (float)(++n);
       mean = mk3(np.x / dv, np.y / dv, np.z / dv);
@@ -2663,7 +2059,6 @@ struct fs_context {
   int nranks = 1, rank = 0;
   DevBuf rows;  // per-lane scratch rows of the lean kernel (LeanRows)
   DevBuf queues;  // per-XCD work-queue counters of the persistent trace kernel
-  DevBuf status;  // kernel status word (Launch::status): bit 0 a walk pool stalled
   uint32_t cus = 0;  // compute units: the persistent grid is one wave per wave slot
 };
 
@@ -2826,63 +2221,44 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
   return FS_OK;
 }
 
-// Waves per SIMD of the default (pooled) lean kernels; other values are A/B builds.
-#ifndef FS_LEAN_WAVES
-#define FS_LEAN_WAVES 6
-#endif
-// Waves per SIMD of the parked-walk (SUSP) kernel. 5 won (+2 % C4) while its
-// spills were 140 B/lane at 6; with the 64-B triangle record 6 wins again
-// (+2 % over 5).
-#ifndef FS_SUSP_WAVES
-#define FS_SUSP_WAVES 6
-#endif
-// Waves per SIMD of the NOWALK kernel (no LDS stack: the LDS rows take 4 KiB
-// per wave, so up to 8 waves fit).
-#ifndef FS_NOWALK_WAVES
-#define FS_NOWALK_WAVES 8
-#endif
-// Waves per SIMD of the POOL kernel (workgroups of one walk wave and three
-// shading waves).
-#ifndef FS_POOL_WAVES
-#define FS_POOL_WAVES 6
-#endif
+// Waves per SIMD (__launch_bounds__) of the three kernel families: the lean
+// kernels (6), the parked-walk kernel (6; 5 waves with 96 VGPRs measured
+// C4 -6.5 %, 7 waves with a 22-entry stack -9.5 %) and the NOWALK kernel (8:
+// no LDS stack, its LDS rows take 4 KiB per wave; 6 waves -4 %, 7 -1.5 %).
+constexpr int kLeanWaves = 6, kSuspWaves = 6, kNowalkWaves = 8;
 
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
 
 // The instantiations of the lean kernel: <COUNT, waves, TEX, SUSP (parked
-// walks), MMAT (material ids in scratch rows)>. Textured scenes never park.
-// Names as rocprofv3 prints the uncounted ones (fs_last_kernel).
+// walks), MMAT (material ids in scratch rows), SOCT (object octree), NOWALK>.
+// Textured scenes never park. Names as rocprofv3 prints the uncounted ones
+// (fs_last_kernel).
 typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, float2*, float4*, float4*, float*, uint32_t*,
                        uint32_t*, DevCounters*);
 struct LeanKernel {
   LeanFn fn;
   const char* name;
   uint32_t waves;  // waves per SIMD (__launch_bounds__)
-  uint32_t wg;     // waves per workgroup: 1, or kPoolWaves (POOL: a walk wave + shading waves)
 };
-template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false, bool POOL = false>
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false>
 LeanKernel lean_kernel(bool count) {
-  constexpr int W = SUSP ? FS_SUSP_WAVES : NOWALK ? FS_NOWALK_WAVES : POOL ? FS_POOL_WAVES : FS_LEAN_WAVES;
+  constexpr int W = SUSP ? kSuspWaves : NOWALK ? kNowalkWaves : kLeanWaves;
   static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
                                   (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
                                   (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ", " +
-                                  (NOWALK ? "true" : "false") + (POOL ? ", true>" : ", false>");
-  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK, POOL>
-                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK, POOL>,
-          name.c_str(), (uint32_t)W, POOL ? dev::kPoolWaves : 1u};
+                                  (NOWALK ? "true>" : "false>");
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK>,
+          name.c_str(), (uint32_t)W};
 }
 // Scenes traced through the object octree take one instantiation that covers
 // textures and any material count (their object loop is per lane anyway).
 // Untextured scenes whose meshes are all small (no BVH walk) take the NOWALK
 // instantiation: no walk stack, shading rows in LDS.
-LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks,
-                       bool pooled) {
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks) {
   if (object_tree) return lean_kernel<true, false, true, true>(count);
   if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
-  if (pooled)
-    return many_materials ? lean_kernel<false, false, true, false, false, true>(count)
-                          : lean_kernel<false, false, false, false, false, true>(count);
   if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
   if (!walks)
     return many_materials ? lean_kernel<false, false, true, false, true>(count)
@@ -2891,10 +2267,7 @@ LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, b
 }
 
 bool valid_options(const fs_options* o, std::string* why) {
-  if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_POOL) *why = "unknown schedule";
-  else if (o->schedule == FS_SCHEDULE_POOL && !o->persist) *why = "the POOL schedule needs persist = 1";
-  else if (o->pool_refill > 64) *why = "pool_refill must be 0..64";
-  else if (o->pool_sync > 1) *why = "pool_sync must be 0 or 1";
+  if (o->schedule < FS_SCHEDULE_AUTO || o->schedule > FS_SCHEDULE_PARKED) *why = "unknown schedule";
   else if (o->samples_per_block < 1 || o->samples_per_block > kChunk) *why = "samples_per_block must be 1..64";
   else if (o->xcd_bands > 2) *why = "xcd_bands must be 0, 1 or 2";
   else if (o->bvh_leaf < 1 || o->bvh_leaf > kMaxLeafCount) *why = "bvh_leaf must be 1..15";
@@ -2944,9 +2317,6 @@ int fs_create(int device, fs_context** out) {
   ctx->cus = cus > 0 ? (uint32_t)cus : 1u;
   FS_HIP(hipMalloc(&ctx->queues.p, 8 * dev::kQueueStride * sizeof(uint32_t)));
   ctx->queues.bytes = 8 * dev::kQueueStride * sizeof(uint32_t);
-  FS_HIP(hipMalloc(&ctx->status.p, 256));
-  ctx->status.bytes = 256;
-  FS_HIP(hipMemset(ctx->status.p, 0, 256));
   *out = ctx.release();
   return FS_OK;
 }
@@ -2958,7 +2328,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
-                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues, &ctx->status})
+                    &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
   ctx->rows.release();
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -2976,8 +2346,6 @@ int fs_options_default(fs_options* o) {
   o->park_lanes_small = 6;  // C3 (38 k and 209 k-face meshes): 4-6 best
   o->park_min_tris = kParkMinTris;
   o->lds_rows = 1;
-  o->pool_refill = 16;
-  o->pool_sync = 1;
   o->samples_per_block = 16;  // persistent waves: C4 +0.7 %, C3 +2 %, C2 +3 % over 64 (8 and 4 no better)
   o->groups = 0;
   o->group_major = 0;
@@ -3241,9 +2609,6 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // triangles and no texture (the textured instantiation has no parking).
   const bool parked = O.schedule == FS_SCHEDULE_PARKED ||
                       (O.schedule == FS_SCHEDULE_AUTO && ctx->has_parking && !ctx->has_textures && !ctx->scene.tree);
-  const bool pooled = O.schedule == FS_SCHEDULE_POOL;
-  if (pooled && (ctx->has_textures || ctx->scene.tree))
-    return fail(FS_ERR_INVALID, "the POOL schedule does not take textured scenes or object-octree scenes");
   if (parked && ctx->has_textures) return fail(FS_ERR_INVALID, "the PARKED schedule does not take textured scenes");
   if (parked && ctx->scene.tree)
     return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
@@ -3309,31 +2674,22 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   LeanRows rows;
   const bool tree = ctx->scene.tree != nullptr;
   const bool mm = ctx->many_materials || tree;
-  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked && !pooled, mm, ctx->scene.tree != nullptr,
-                                   ctx->has_walks || !O.lds_rows, pooled);
+  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr,
+                                   ctx->has_walks || !O.lds_rows);
   // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
-  // K.waves waves per SIMD), never more than the launch has blocks; POOL
-  // workgroups hold K.wg waves, K.wg - 1 of them shading (taking blocks).
+  // K.waves waves per SIMD), never more than the launch has blocks.
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
-  const uint64_t shade_per_wg = K.wg > 1 ? K.wg - 1 : 1;
-  auto grid_for = [&](uint64_t nb) {  // workgroups of a launch of nb blocks
-    if (!O.persist) return nb;
-    return std::min<uint64_t>(wave_slots / K.wg, (nb + shade_per_wg - 1) / shade_per_wg);
-  };
+  auto grid_for = [&](uint64_t nb) { return O.persist ? std::min<uint64_t>(wave_slots, nb) : nb; };
   if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
   // On an allocation failure the launches shrink (G halved) until the rows fit.
-  while (blocks && (rc = lean_rows(ctx, grid_for(blocks * G) * shade_per_wg * kBlock, blocks * G * kBlock, chunk,
-                                   &rows, ctx->has_textures || tree, mm))) {
+  while (blocks && (rc = lean_rows(ctx, grid_for(blocks * G) * kBlock, blocks * G * kBlock, chunk, &rows,
+                                   ctx->has_textures || tree, mm))) {
     if (G == 1 || O.groups) return rc;
     G = (G + 1) / 2;
     (void)hipGetLastError();  // clear the failed hipMalloc's error state
   }
   ctx->last_kernel = K.name;
   L.persist = O.persist;
-  L.pool_refill = O.pool_refill;
-  L.pool_sync = O.pool_sync;
-  L.status = (uint32_t*)ctx->status.p;
-  FS_HIP(hipMemsetAsync(ctx->status.p, 0, 4, ctx->stream));
   for (uint32_t done = 0; done < params->spp && blocks;) {
     L.sample_base = params->sample_base + done;
     L.spp = std::min(chunk, params->spp - done);
@@ -3344,7 +2700,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
     const uint32_t grid = (uint32_t)grid_for(L.nblocks);
     if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
-    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock * K.wg), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
+    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
                        rows.tex, rows.rad, rows.mat, (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
     hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
     FS_HIP(hipGetLastError());
@@ -3353,21 +2709,12 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   return FS_OK;
 }
 
-// The kernels' status word after the stream has drained (a stalled walk
-// pool's watchdog ends the kernel with a bad frame instead of hanging).
-int check_status(fs_context* ctx) {
-  uint32_t st = 0;
-  FS_HIP(hipMemcpy(&st, ctx->status.p, 4, hipMemcpyDeviceToHost));
-  if (st & 1u) return fail(FS_ERR_DEVICE, "walk pool stalled (watchdog): the frame is invalid");
-  return FS_OK;
-}
-
 int fs_synchronize(fs_context* ctx) {
   if (!ctx) return fail(FS_ERR_INVALID, "null context");
   int rc;
   if ((rc = set_device(ctx))) return rc;
   FS_HIP(hipStreamSynchronize(ctx->stream));
-  return check_status(ctx);
+  return FS_OK;
 }
 
 const char* fs_last_kernel(fs_context* ctx) { return ctx ? ctx->last_kernel : ""; }
@@ -3385,7 +2732,7 @@ int fs_last_render_ms(fs_context* ctx, float* ms) {
   if ((rc = set_device(ctx))) return rc;
   FS_HIP(hipEventSynchronize(ctx->ev1));
   FS_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
-  return check_status(ctx);
+  return FS_OK;
 }
 
 int fs_read_counters(fs_context* ctx, fs_counters* out) {
@@ -3405,16 +2752,6 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->small_tri_loads = c.small_tri_loads;
   out->lane_object_loads = c.lane_object_loads;
 #ifdef FS_PHASE_PROF
-#ifdef FS_ROOT_STATS
-  {
-    unsigned long long rs[8] = {};
-    if (hipMemcpyFromSymbol(rs, HIP_SYMBOL(dev::g_root_stats), sizeof(rs)) == hipSuccess)
-      std::fprintf(stderr, "[fs root] culls %llu exact %llu (par %llu pair %llu near-1 %llu near-best %llu; start inside %llu)\n",
-                   rs[0], rs[1], rs[2], rs[3], rs[4], rs[5], rs[6]);
-    const unsigned long long zero[8] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(dev::g_root_stats), zero, sizeof(zero));
-  }
-#endif
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "
                "shade %llu unwind %llu - iters %llu total %llu\n",
@@ -3431,11 +2768,6 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                c.phase[14], (double)c.phase[26] / (c.phase[8] ? c.phase[8] : 1),
                (double)c.phase[27] / (c.phase[8] ? c.phase[8] : 1), (double)c.phase[28] / (c.phase[8] ? c.phase[8] : 1),
                (double)c.phase[29] / (c.phase[28] ? c.phase[28] : 1));
-  std::fprintf(stderr, "[fs hist] node visits per segment: 0:%llu 1-4:%llu 5-8:%llu 9-16:%llu 17-32:%llu 33-64:%llu "
-               "65-128:%llu >128:%llu\n", c.phase[16], c.phase[17], c.phase[18], c.phase[19], c.phase[20],
-               c.phase[21], c.phase[22], c.phase[23]);
-  std::fprintf(stderr, "[fs seq] per-call wave max of lane node visits %llu (node trips %llu), of lane leaf tests "
-               "%llu (leaf trips %llu)\n", c.phase[24], c.phase[10], c.phase[25], c.phase[11]);
 #endif
   return FS_OK;
 }

@@ -100,9 +100,6 @@ struct Launch {
   uint64_t seed;
   uint32_t nblocks;  // blocks of the launch: owned tiles x micro-tiles x groups
   uint32_t persist;  // 1: persistent waves pull blocks from per-XCD queues; 0: one wave per block
-  uint32_t pool_refill;  // POOL: the walk wave refills once at most this many lanes still walk
-  uint32_t pool_sync;    // POOL: shading waves wait for their walks within the iteration (1) or go on (0)
-  uint32_t* status;      // bit 0: a walk pool stalled (watchdog); read back by fs_synchronize
 };
 
 }  // namespace fs

@@ -54,12 +54,7 @@ FS_HD float length(f3 a) { return fsqrt(dot(a, a)); }       // vector3.h:301
 FS_HD f3 normalize(f3 a) {                                  // vector3.h:181-191
   float l = length(a);
   if (l == 0.0f) l = 1.0f;
-#if defined(FS_MEAS_FASTDIV) && defined(__HIP_DEVICE_COMPILE__)  // measurement builds only: frames differ
-  const float rl = __builtin_amdgcn_rcpf(l);
-  return f3{a.x * rl, a.y * rl, a.z * rl};
-#else
   return f3{a.x / l, a.y / l, a.z / l};
-#endif
 }
 FS_HD f3 reflect(f3 v, f3 n) { return v - n * (dot(n, v) * (1.0f + 1.0f)); }  // vector3.h:208
 FS_HD f3 refract(f3 v, f3 n, float index) {                                   // vector3.h:213-222

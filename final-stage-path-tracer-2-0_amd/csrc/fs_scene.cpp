@@ -144,7 +144,6 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
   t->plane[1] = pl.y;
   t->plane[2] = pl.z;
   t->plane[3] = pl.w;
-#if FS_TRI64
   const float P[3] = {p0.x, p0.y, p0.z}, A[3] = {v0.x, v0.y, v0.z}, B[3] = {v1.x, v1.y, v1.z};
   const int ia = axis == 0 ? 1 : 0, ib = axis == 2 ? 1 : 2;
   t->p1[0] = P[ia];
@@ -154,18 +153,6 @@ void fill_tri(DevTri* t, f3 p0, f3 p1, f3 p2, f4 pl) {
   t->v1[0] = B[ia];
   t->v1[1] = B[ib];
   t->face_axis = (t->face_axis & 0x3FFFFFFFu) | (axis << 30);
-#else
-  t->p1[0] = p0.x;
-  t->p1[1] = p0.y;
-  t->p1[2] = p0.z;
-  t->v0[0] = v0.x;
-  t->v0[1] = v0.y;
-  t->v0[2] = v0.z;
-  t->v1[0] = v1.x;
-  t->v1[1] = v1.y;
-  t->v1[2] = v1.z;
-  t->axis = axis;
-#endif
 }
 
 constexpr int kMaxBins = 64;
@@ -950,11 +937,7 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
       }
       DevTri& t = mtris[f];
       std::memset(&t, 0, sizeof(t));
-#if FS_TRI64
       t.face_axis = f;
-#else
-      t.face = f;
-#endif
       if (need) {
         f3 p0 = verts[vi[0]], p1 = verts[vi[1]], p2 = verts[vi[2]];
         fill_tri(&t, p0, p1, p2, plane_np(calc_normal(p0, p1, p2), p0));  // mesh.cpp:136-146

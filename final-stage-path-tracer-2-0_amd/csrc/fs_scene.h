@@ -67,10 +67,7 @@ FS_HD uint32_t leaf_word(uint32_t count, uint32_t first) {
   return kLeafBit | (count << kLeafCountShift) | first;
 }
 FS_HD uint32_t leaf_count(uint32_t w) { return (w >> kLeafCountShift) & 0xFu; }
-#ifndef FS_STACK
-#define FS_STACK 24  // (other values are A/B builds: the LDS stack bounds the waves per CU)
-#endif
-constexpr uint32_t kTraversalStack = FS_STACK;  // BVH depth bound (builder enforces)
+constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces); the LDS stack bounds the waves per CU
 constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
 // Triangle record: the operands of the reference test (intersect.cpp:357-419)
@@ -79,10 +76,6 @@ constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 // plane axis zeroed, intersect.cpp:96-129), their dot products and
 // 1/(d00*d11 - d01*d01) (:168-173), the face plane (mesh.cpp:136-146,
 // reversed winding) and the face index (tie-break).
-#ifndef FS_TRI64
-#define FS_TRI64 1
-#endif
-#if FS_TRI64
 // 64 B: the planar map zeroes one axis, so p1, v0 and v1 keep only the two
 // others, (a, b) = (axis == 0 ? y : x, axis == 2 ? y : z); face and axis
 // share a word (face | axis << 30).
@@ -98,24 +91,6 @@ struct DevTri {
 static_assert(sizeof(DevTri) == 64, "DevTri layout");
 constexpr uint32_t kSamePlaneBit = 0x80000000u;
 inline uint32_t tri_face_host(const DevTri& t) { return t.face_axis & 0x3FFFFFFFu; }
-#else
-// 80 B: full 3-vectors (A/B builds with -DFS_TRI64=0).
-struct DevTri {
-  float p1[3];
-  uint32_t face;
-  float v0[3];
-  float d00;
-  float v1[3];
-  float d01;
-  float d11;
-  float inv;
-  uint32_t axis;  // zeroed component of the planar map (0=x, 1=y, 2=z)
-  uint32_t mesh_obj;
-  float plane[4];
-};
-static_assert(sizeof(DevTri) == 80, "DevTri layout");
-inline uint32_t tri_face_host(const DevTri& t) { return t.face; }
-#endif
 
 // The reference's scene object octree (SceneBvh, scene.cpp:11-133), built
 // when Scene::Optimize ran and the scene has >= 182 objects (scene.cpp:216-

@@ -98,12 +98,11 @@ class fs_options(C.Structure):
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
                 ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
-                ("lds_rows", C.c_uint32), ("pool_refill", C.c_uint32),
-                ("pool_sync", C.c_uint32)]
+                ("lds_rows", C.c_uint32)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
-SCHEDULES = {"auto": 0, "lean": 1, "parked": 2, "pool": 3}  # fs_schedule
+SCHEDULES = {"auto": 0, "lean": 1, "parked": 2}  # fs_schedule
 NODE_LAYOUTS = {"depth_first": 0, "pairs": 1}
 
 # Exported symbols of include/fs_trace.h, with their ctypes signatures.
@@ -193,12 +192,17 @@ def _bind(lib, table):
     return lib
 
 
+def gpu_lib_path():
+    """The libfsgpu.so this process loads: the in-tree product build, or the
+    measurement build FSAMD_GPU_LIB names (libfsgpu_prof.so, A/B builds)."""
+    return os.environ.get("FSAMD_GPU_LIB") or os.path.join(PKG_DIR, "libfsgpu.so")
+
+
 def gpu_lib():
     """libfsgpu.so (HIP kernels + C ABI). Raises if it has not been built."""
     global _gpu
     if _gpu is None:
-        # FSAMD_GPU_LIB selects a measurement build (libfsgpu_prof.so).
-        path = os.environ.get("FSAMD_GPU_LIB") or os.path.join(PKG_DIR, "libfsgpu.so")
+        path = gpu_lib_path()
         if not os.path.exists(path):
             raise FsError(f"{path} missing: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
         _gpu = _bind(C.CDLL(path, mode=C.RTLD_GLOBAL), GPU_SYMBOLS)

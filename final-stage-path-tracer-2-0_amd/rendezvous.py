@@ -154,6 +154,13 @@ class FileGroup:
         self._done(seq)
         return [list(struct.unpack(f"<{len(got[r]) // 8}d", got[r])) for r in range(self.world)]
 
+    def allgather_bytes(self, data: bytes) -> list:
+        """Every rank's bytes, in rank order."""
+        seq = self.seq
+        got = self._op(bytes(data), range(self.world))
+        self._done(seq)
+        return [got[r] for r in range(self.world)]
+
     def abort(self) -> None:
         """Clean-up of a rank that fails: an "abort" marker for the others,
         then its own files go; rank 0 removes the directory."""

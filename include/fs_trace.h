@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 5
+#define FS_ABI_VERSION 6
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -230,9 +230,7 @@ typedef enum fs_schedule {
   FS_SCHEDULE_AUTO = 0,   /* PARKED when the scene has a mesh of >= park_min_tris
                              triangles and no texture, else LEAN */
   FS_SCHEDULE_LEAN = 1,   /* path-regeneration megakernel, pooled (pixel, sample) tasks */
-  FS_SCHEDULE_PARKED = 2, /* LEAN + BVH walks of large meshes park when few lanes walk */
-  FS_SCHEDULE_POOL = 3    /* workgroups of 4 waves: one walks every BVH for the other three
-                             (an LDS pool of segments), which shade; needs persist = 1 */
+  FS_SCHEDULE_PARKED = 2  /* LEAN + BVH walks of large meshes park when few lanes walk */
 } fs_schedule;
 
 #define FS_NODE_LAYOUT_DEPTH_FIRST 0u
@@ -268,11 +266,6 @@ typedef struct fs_options {
   uint32_t park_lanes_small;   /* PARKED: park_lanes for parkable meshes under 2^19 triangles (6) */
   uint32_t lds_rows;           /* 1: scenes without BVH walks (every mesh small, no texture) run
                                   the NOWALK kernel, shading rows in LDS (1); 0 the LEAN kernel */
-  uint32_t pool_refill;        /* POOL: the walk wave takes pending walks once at most this many
-                                  of its lanes still walk (16; 0..64) */
-  uint32_t pool_sync;          /* POOL: 1 a shading wave sleeps until the walks it posted are done
-                                  and finishes those segments in the same iteration (1); 0 the
-                                  lanes wait for the next iteration */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */

@@ -7,6 +7,8 @@ import multiprocessing as mp
 import os
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "final-stage-path-tracer-2-0_amd"))
@@ -126,3 +128,91 @@ def test_rendezvous_abort_wakes_waiting_ranks(tmp_path):
     th.join(10)
     assert not th.is_alive()
     assert "rank 0 aborted" in seen["err"] and seen["s"] < 5
+
+
+def test_roofline_bound_comes_from_measured_fractions():
+    import bench
+
+    # C3 of round 3: modelled bytes said 0.88 of HBM, the PMC said 0.25 traffic,
+    # 0.33 VALU issue and 54 % of wave cycles waiting: latency
+    assert bench.roofline_bound(0.25, 0.33, 0.54) == "latency"
+    assert bench.roofline_bound(0.25, 0.33, 0.30) == "valu"
+    assert bench.roofline_bound(0.70, 0.33, 0.54) == "hbm"
+    assert bench.roofline_bound(0.30, 0.62, 0.45) == "valu"
+    assert bench.roofline_bound(None, 0.5, 0.5) is None  # unmeasured
+
+
+def _pmc_file(root, build, kernel="render_kernel_lean<false, 6, false, true, false, false, false>"):
+    import json
+
+    os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+    pm = {"kernel": "void fs::dev::" + kernel, "code_object_sha256": build, "hbm_bytes_per_sample": 1400.0,
+          "valu_insts_per_sample": 300.0, "clock_ghz": 2.4, "valu_lane_util": 0.29, "wait_any_frac": 0.47}
+    json.dump(pm, open(os.path.join(root, "profiles", "pmc_c4_1920x1080.json"), "w"))
+
+
+def test_pmc_replay_only_onto_the_same_build(tmp_path, monkeypatch):
+    import bench
+
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    kernel = "render_kernel_lean<false, 6, false, true, false, false, false>"
+    _pmc_file(str(tmp_path), "a" * 64)
+    c = {"node_visits": 800, "tri_tests": 100, "small_tri_loads": 10, "object_loads": 5, "segments": 37,
+         "samples": 10, "prim_tests": 30}
+    args = ("c4", 1920, 1080, 1024, c, 8, [1100.0], kernel, 1, 1024)
+    same = bench.make_roofline(*args, build="a" * 64)
+    assert same["traffic"] and same["valu"] and same["pmc_replay_refused"] is None
+    assert same["bound"] == "latency" and same["bound_source"].startswith("measured")
+    assert "valu_busy_rocprof" not in same["valu"]
+    other = bench.make_roofline(*args, build="b" * 64)  # same kernel name, another build
+    assert other["traffic"] is None and other["valu"] is None
+    assert "build" in other["pmc_replay_refused"] and other["bound_source"].startswith("unmeasured")
+    assert other["frac"] == same["frac"]  # the algorithmic-byte frac does not depend on the replay
+    _pmc_file(str(tmp_path), "a" * 64, kernel="render_kernel_lean<false, 6, false, false, false, false, false>")
+    assert bench.make_roofline(*args, build="a" * 64)["traffic"] is None  # another kernel
+
+
+def _gather_rank(rank, world, path, q, corrupt):
+    import numpy as np
+
+    import bench
+    import rendezvous
+    import tiles
+
+    W, H, TS = 150, 70, 16
+    rng = np.random.default_rng(3)
+    full = {"color": rng.random((H, W, 3), dtype=np.float32), "count": rng.integers(1, 9, (H, W)).astype(np.uint32),
+            "normal": rng.random((H, W, 3), dtype=np.float32), "depth": rng.random((H, W), dtype=np.float32),
+            "material": rng.integers(0, 2**63, (H, W)).astype(np.uint64)}
+    own = tiles.owner_map(W, H, world, TS)
+    # this rank's frame: its own tiles as rendered; rank 0's also the gathered ones
+    mine = {k: np.where((own == rank).reshape(own.shape + (1,) * (v.ndim - 2)), v, 0).astype(v.dtype)
+            for k, v in full.items()}
+    if rank == 0:
+        mine = {k: v.copy() for k, v in full.items()}
+        if corrupt:
+            mine["color"][own == 1] += np.float32(1e-3)  # one rank's tiles arrive damaged
+    g = rendezvous.FileGroup(rank, world, path=path, timeout=60)
+    res = bench.gather_check(g, rank, world, lambda k: tiles.pack_words(mine, W, H, k, world, TS).tobytes())
+    out = bench.make_record(_args(), world, 1.0, STATS, ROOF, None, res) if rank == 0 else res
+    g.close()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_multi_gpu_line_verifies_the_gathered_frame(tmp_path, corrupt):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_rank, args=(r, world, str(tmp_path / "rdzv"), q, corrupt))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    ranks = got[0]["ranks"]
+    assert ranks["gather_ok"] is (not corrupt)
+    assert ranks["gather_mismatch_ranks"] == ([1] if corrupt else [])
+    assert len(ranks["tile_digests"]) == world and got[1] == {}

@@ -16,6 +16,7 @@ import pytest
 
 import fsamd
 import oracle_py
+import tiles
 from conftest import GOLDEN, load_scene
 from descbuild import DescBuilder, cornell_room
 
@@ -139,7 +140,7 @@ def zoo(frost=0.0):
     return b
 
 
-@pytest.mark.parametrize("schedule", ["auto", "parked", "pool"])
+@pytest.mark.parametrize("schedule", ["auto", "parked"])
 def test_material_and_object_zoo_bit_exact(schedule, gpu_renderer):
     """Every material and object kind. The lean kernel applies Material::Sample
     as straight-line selects, the parked-walk kernel as a per-kind switch:
@@ -485,6 +486,11 @@ def test_tile_exchange_rebuilds_single_gpu_frame(nranks, root, scene_dir, gpu_re
         f = r.frame(W, H)
         p = r.render(cam, f, spp=spp, tile_offset=k, tile_stride=nranks)
         packs.append(r.pack(f, p))
+        # the 40-B/pixel format is the one tiles.pack_words restates (the gloo test's)
+        planes = {"color": f.read(fsamd.PLANE_COLOR), "count": f.read(fsamd.PLANE_COUNT),
+                  "normal": f.read(fsamd.PLANE_NORMAL), "depth": f.read(fsamd.PLANE_DEPTH),
+                  "material": f.read(fsamd.PLANE_MATERIAL)}
+        np.testing.assert_array_equal(packs[-1], tiles.pack_words(planes, W, H, k, nranks))
         if k == root:
             root_frame, root_params = f, p
         else:
@@ -563,9 +569,6 @@ OPTION_VARIANTS = [
     {"schedule": "parked", "park_min_tris": 1},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes": 63, "park_lanes_small": 63},
     {"schedule": "parked", "park_min_tris": 1, "park_lanes_small": 1},
-    {"schedule": "pool"},
-    {"schedule": "pool", "pool_refill": 0, "pool_sync": 0},
-    {"schedule": "pool", "pool_refill": 64, "small_mesh_tris": 0},
     {"samples_per_block": 64},
     {"samples_per_block": 7},
     {"xcd_bands": 0},
@@ -649,26 +652,6 @@ def test_bench_scale_parity(name, schedule, scene_dir, gpu_renderer):
     assert_parity(out, ref, exact=False)
     for p in (fsamd.PLANE_MATERIAL, fsamd.PLANE_NORMAL, fsamd.PLANE_DEPTH):  # the last sample's AOVs
         assert diff[p] <= 1e-3 * W * H, diff
-
-
-@pytest.mark.parametrize("name", ["c4", "c3"])
-def test_pool_schedule_matches_parked(name, scene_dir, gpu_renderer):
-    """The POOL schedule (a walk wave per workgroup walks every BVH for three
-    shading waves, through an LDS pool of segments) renders the PARKED
-    schedule's frame bit for bit on every plane: the walks are the same
-    operations on another lane. C4 and C3 over the bench camera at
-    480x270 x 8 spp, plus the no-refill and refill-at-every-pass settings."""
-    s = load_scene(name, scene_dir)
-    cam = s.camera(0)
-    W, H, spp = 480, 270, 8
-    gpu_renderer.set_options(schedule="parked")
-    ref = gpu_render(gpu_renderer, s, cam, W, H, spp)
-    for refill, sync in ((16, 1), (0, 0), (64, 1), (16, 0)):
-        gpu_renderer.set_options(schedule="pool", pool_refill=refill, pool_sync=sync)
-        out = gpu_render(gpu_renderer, s, cam, W, H, spp)
-        assert gpu_renderer.last_kernel().endswith("true>"), gpu_renderer.last_kernel()
-        for p in ref:
-            np.testing.assert_array_equal(out[p], ref[p], err_msg=f"plane {p}, refill {refill}, sync {sync}")
 
 
 # ---- scenes with more than 255 materials (material ids in scratch rows) ----

@@ -187,6 +187,13 @@ def test_generated_scene_sizes(scene_dir):
     assert f.shape == (10000, 3) and v.shape == (51 * 100, 3)
     path, ntri = scenes.write_c3(os.path.join(scene_dir, "c3_count"))
     assert abs(ntri - 250_000) / 250_000 < 0.01
+    # SURVEY Appendix A's calibration probe: the C1 room (6 meshes + 2 boxes) and one blob, no analytic objects
+    fsamd.reset_main_rng()
+    s = fsamd.HostScene.load(scenes.write_probe(os.path.join(scene_dir, "probe_count"), nu=40, nv=20))
+    d = s.desc().contents
+    kinds = [d.objects[i].kind for i in range(d.num_objects)]
+    assert kinds == [fsamd.OBJ_MESH] * 7
+    assert sum(d.meshes[i].num_triangles for i in range(d.num_meshes)) == 40 * 20 * 2 + 36
 
 
 def test_parallel_bvh_build_is_reproducible(scene_dir, monkeypatch):

@@ -20,15 +20,15 @@ LIMITS = {
     # PARKED schedule: C3 and C4 (the bench kernel). 44 -> 60 B/lane with the
     # lane-major rows and the unrolled backward pass (C4 +3.5 % all the same,
     # profiles/r03/ab_lrows.log)
-    "render_kernel_lean<false, 6, false, true, false, false, false, false>": (60, 21, 80),
+    "render_kernel_lean<false, 6, false, true, false, false, false>": (60, 21, 80),
     # LEAN schedule: scenes with BVH walks and no large mesh. 16 -> 20 B/lane
     # without the traversal s_setprio (FS_TRAV_PRIO 0: C4 +1.1 %, C3 +0.3 % on
     # the parked-walk kernel, profiles/r03/ab_sched.log; no bench config runs LEAN)
-    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (20, 12, 80),
+    "render_kernel_lean<false, 6, false, false, false, false, false>": (20, 12, 80),
     # LEAN without walks (NOWALK: every mesh small, shading rows in LDS, 8 waves
     # per SIMD): C1 and C2. 32 -> 44 B/lane with the straight-line mesh-root
     # cull on the segment's slopes (C2 +6.7 % all the same, profiles/r03/ab_root_tol.log)
-    "render_kernel_lean<false, 8, false, false, false, false, true, false>": (44, 27, 64),
+    "render_kernel_lean<false, 8, false, false, false, false, true>": (44, 27, 64),
 }
 
 
@@ -53,10 +53,9 @@ def test_trace_kernel_spills_within_budget(kernel, resources):
 def test_every_product_kernel_fits_its_wave_count(resources):
     """render_kernel_lean<COUNT, waves, ...>: the VGPRs and LDS of a product
     kernel fit `waves` waves per SIMD (512 VGPRs per lane and 160 KiB of LDS
-    per CU of 4 SIMDs; a POOL workgroup is 4 waves)."""
+    per CU of 4 SIMDs)."""
     for name, r in resources.items():
         if name.startswith("render_kernel_lean<false"):
             waves = int(name.split(", ")[1])
-            wg = 4 if name.endswith("true>") else 1  # POOL: workgroups of 4 waves
             assert r["vgpr_count"] <= 512 // waves // 8 * 8, (name, r)
-            assert r["group_segment_fixed_size"] <= 160 * 1024 * wg // (4 * waves), (name, r)
+            assert r["group_segment_fixed_size"] <= 160 * 1024 // (4 * waves), (name, r)

@@ -1,0 +1,91 @@
+#!/bin/bash
+# The one GPU-box runner (run from the repo root under gpurun). Every step runs
+# under its own time limit; the first failing step ends the run.
+#
+# usage: bash tools/gpu_run.sh ROUND STEP [STEP ...]
+#   tests[:PYTEST_ARGS]          pytest -m gpu (log + parity records in gpurun_out/ROUND)
+#   smoke                        __graft_entry__.smoke()
+#   bench:SCENE[:WxH[:STEPS]]    one bench.py line -> bench_SCENE_WxH.json (C4 1080p adds the CPU baseline)
+#   prof[:SCENE]                 rocprofv3 --kernel-trace --stats of the bench command -> prof_SCENE/
+#   pmc:SCENE:WxH:SPP            PMC passes (one counter group each) + tools/pmc_summary.py
+#                                -> pmc_SCENE_WxH.json, stamped with the code object's digest
+#   ab:VARIANTS:SCENES:SPP:ROUNDS   tools/perf_ab.py (fs_options A/B in one process)
+#   libab:LIBS:SCENES:SPP:ROUNDS    alternating processes over in-tree builds (space-separated .so names)
+#   phase:SCENES:SPP             per-phase cycle split (needs the in-tree libfsgpu_prof.so)
+set -o pipefail
+R=$1
+shift
+OUT=gpurun_out/$R
+mkdir -p $OUT
+export TMPDIR=/tmp
+fail() { echo "step $1 failed (rc $2)"; [ -n "$3" ] && tail -25 "$3"; exit 1; }
+
+for step in "$@"; do
+  IFS=: read -r name a1 a2 a3 a4 <<< "$step"
+  echo "== $step ($(date +%T))"
+  case $name in
+    tests)
+      rm -f gpurun_out/parity_records.jsonl
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread $a1 \
+        > $OUT/pytest_gpu.log 2>&1 || fail $step $? $OUT/pytest_gpu.log
+      [ -f gpurun_out/parity_records.jsonl ] && mv gpurun_out/parity_records.jsonl $OUT/
+      tail -2 $OUT/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+        || fail $step $? $OUT/smoke.log
+      tail -2 $OUT/smoke.log ;;
+    bench)
+      sc=${a1:-c4}; wh=${a2:-1920x1080}; w=${wh%x*}; h=${wh#*x}; st=${a3:-3}
+      cpu=--no-cpu; [ "$sc$wh" = c41920x1080 ] && cpu=
+      f=$OUT/bench_${sc}_${wh}
+      timeout -k 10 600 python bench.py --scene $sc --width $w --height $h --steps $st $cpu > $f.json 2> $f.err \
+        || fail $step $? $f.err
+      cut -c1-220 $f.json ;;
+    prof)
+      sc=${a1:-c4}
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$sc -o trace -- \
+        python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu > $OUT/prof_$sc.json 2> $OUT/prof_$sc.err \
+        || fail $step $? $OUT/prof_$sc.err
+      find $OUT/prof_$sc -name "*kernel_stats.csv" -exec cut -c1-160 {} \; ;;
+    pmc)
+      sc=$a1; wh=$a2; w=${wh%x*}; h=${wh#*x}; spp=$a3
+      d=$OUT/pmc_${sc}_${wh}
+      mkdir -p $d
+      cmd="python3 bench.py --scene $sc --steps 1 --warmup 0 --spp $spp --no-cpu --width $w --height $h"
+      i=0
+      for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH" \
+                 "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM" \
+                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" \
+                 "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i+1))
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $d/p$i -o pmc -- $cmd \
+          > $d/p$i.out 2> $d/p$i.err || fail "$step pass $i" $? $d/p$i.err
+      done
+      kern=$(python3 -c "import json; print([json.loads(l) for l in open('$d/p1.out') if l.startswith('{')][-1]['roofline']['kernel'])") \
+        || fail $step $?
+      python3 tools/pmc_summary.py $d "$kern" $OUT/pmc_${sc}_${wh}.json "$sc ${wh} x $spp spp, one launch" \
+        $((w * h * spp)) > $d/summary.log 2>&1 || fail $step $? $d/summary.log
+      grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $OUT/pmc_${sc}_${wh}.json ;;
+    ab)
+      log=$OUT/ab_$(date +%H%M%S).log
+      timeout -k 10 900 python tools/perf_ab.py "$a1" "$a2" ${a3:-256} ${a4:-2} > $log 2>&1 || fail $step $? $log
+      grep -E "variant|differs|md5" $log ;;
+    libab)
+      log=$OUT/libab_$(date +%H%M%S).log
+      for i in $(seq 1 ${a4:-2}); do
+        for L in $a1; do
+          echo "== $L" >> $log
+          FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/$L timeout -k 10 300 \
+            python tools/perf_ab.py default "$a2" ${a3:-256} 1 >> $log 2>&1 || fail $step $? $log
+        done
+      done
+      grep -E "^==|variant" $log ;;
+    phase)
+      FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/libfsgpu_prof.so timeout -k 10 600 \
+        python tools/phase_prof.py "$a1" ${a2:-64} > $OUT/phase.log 2>&1 || fail $step $? $OUT/phase.log
+      grep -E "==|phase|trips" $OUT/phase.log ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== all steps done ($(date +%T))"

@@ -9,10 +9,15 @@ counted by both, so this is L2-miss (fabric) traffic, an upper bound on HBM.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import isa_guard  # noqa: E402
 
 
 def kernel_durations(pmc_dir, kname):
@@ -44,6 +49,10 @@ def main():
         raise SystemExit(f"no dispatches of {kname!r} under {pmc_dir}")
     avg = {c: sum(d.values()) / len(d) for c, d in vals.items()}
     res = dict(meta)
+    # the build the counters belong to: bench.py replays this summary only onto
+    # a run of the same code object (bench.build_id)
+    lib = os.environ.get("FSAMD_GPU_LIB") or os.path.join(ROOT, "final-stage-path-tracer-2-0_amd", "libfsgpu.so")
+    res["code_object_sha256"] = hashlib.sha256(isa_guard.code_object(lib)).hexdigest()
     res["dispatches"] = {c: len(d) for c, d in vals.items()}
     res["counters_avg_per_dispatch"] = {c: round(v, 3) for c, v in sorted(avg.items())}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
