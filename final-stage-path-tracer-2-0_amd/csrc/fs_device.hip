@@ -30,6 +30,9 @@
 // lane-major HBM shading rows, object heads as one scalar load, 12-B radiance
 // records. The only remaining switch is FS_PHASE_PROF (the profiling build,
 // libfsgpu_prof.so).
+#ifndef FS_BVH4  // round-4 A/B: walks over 4-wide nodes collapsed from the BVH2 (1)
+#define FS_BVH4 0
+#endif
 
 namespace fs {
 namespace dev {
@@ -876,14 +879,64 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   bool susp = false;
   while ((w != kNone || leaf) && !(SUSP && susp)) {
     while (!(w & kLeafBit) && w != kNone) {
-      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
-      float4 X = q[0], Y = q[1], Z = q[2];
-      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       if (COUNT) tally.nodes++;
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.node_trips);
       tally.lane_nodes++;
 #endif
+#if FS_BVH4
+      {
+        // Four child boxes per trip. Hit children get keys (entry time bits,
+        // child index in the low 2 bits; a miss 0xFFFFFFFF), sorted by a
+        // 5-comparator network: the nearest goes on, the others are pushed
+        // farthest first. The collapse keeps every walk's stack within
+        // kTraversalStack entries, and the writes past the pushed entries
+        // stay below it too (sp + pushes of this node <= the bound).
+        const float4* q = reinterpret_cast<const float4*>(S.nodes4 + w);
+        const float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
+        const uint4 Cw = reinterpret_cast<const uint4*>(q)[6];
+        const int tl = __float_as_int(tmax_lim);
+        auto key = [&](float lx, float hx, float ly, float hy, float lz, float hz, uint32_t i) -> uint32_t {
+          const float a = fmaf(lx, ix, ox), b = fmaf(hx, ix, ox);
+          const float c = fmaf(ly, iy, oy), e = fmaf(hy, iy, oy);
+          const float g = fmaf(lz, iz, oz), k = fmaf(hz, iz, oz);
+          const float n = fmaxf(fmaxf(fminf(a, b), fminf(c, e)), fmaxf(fminf(g, k), -1e-6f));
+          const float f = fminf(fminf(fmaxf(a, b), fmaxf(c, e)), __int_as_float(min(__float_as_int(fmaxf(g, k)), tl)));
+          return n <= f ? ((__float_as_uint(n) & 0x7FFFFFFCu) | i) : 0xFFFFFFFFu;
+        };
+        uint32_t k0 = key(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, 0u);
+        uint32_t k1 = key(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, 1u);
+        uint32_t k2 = key(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, 2u);
+        uint32_t k3 = key(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, 3u);
+        auto cs = [](uint32_t& a, uint32_t& b) {
+          const uint32_t lo = min(a, b), hi = max(a, b);
+          a = lo;
+          b = hi;
+        };
+        cs(k0, k1);
+        cs(k2, k3);
+        cs(k0, k2);
+        cs(k1, k3);
+        cs(k1, k2);
+        auto sel = [&](uint32_t k) {
+          return (k & 2u) ? ((k & 1u) ? Cw.w : Cw.z) : ((k & 1u) ? Cw.y : Cw.x);
+        };
+        if (k0 == 0xFFFFFFFFu) {
+          w = sp ? stk[--sp * kBlock] : kNone;
+        } else {
+          w = sel(k0);
+          stk[sp * kBlock] = sel(k3);
+          sp += k3 != 0xFFFFFFFFu;
+          stk[sp * kBlock] = sel(k2);
+          sp += k2 != 0xFFFFFFFFu;
+          stk[sp * kBlock] = sel(k1);
+          sp += k1 != 0xFFFFFFFFu;
+        }
+      }
+#else
+      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+      float4 X = q[0], Y = q[1], Z = q[2];
+      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       bool h0, h1;
       float t0, t1;
       {
@@ -917,6 +970,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       } else {
         w = sp ? stk[--sp * kBlock] : kNone;
       }
+#endif
       if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
         leaf = w;
         w = sp ? stk[--sp * kBlock] : kNone;
@@ -2036,7 +2090,7 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
+  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
       pack_recv, range_io, tree, tree_objs;
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
@@ -2326,7 +2380,7 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
@@ -2443,9 +2497,32 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
                    D.num_tris, res.build_ms, res.levels, res.nodes_used, res.max_depth);
     D = DeferredMesh();  // release the host copies
   }
+#if FS_BVH4
+  {  // every walked mesh's BVH2 collapsed into 4-wide nodes (host; the device-built trees come back first)
+    std::vector<BvhNode> all(ctx->nodes.bytes / sizeof(BvhNode));
+    FS_HIP(hipMemcpy(all.data(), ctx->nodes.p, all.size() * sizeof(BvhNode), hipMemcpyDeviceToHost));
+    std::vector<Bvh4Node> n4;
+    std::vector<std::pair<int32_t, uint32_t>> done;  // BVH2 root -> BVH4 root (meshes shared by objects)
+    for (DevObject& o : P.objects) {
+      if (o.kind != FS_OBJ_MESH || !o.i2 || o.i3) continue;
+      uint32_t r4 = 0xFFFFFFFFu;
+      for (auto& d : done)
+        if (d.first == o.i0) r4 = d.second;
+      if (r4 == 0xFFFFFFFFu) {
+        r4 = collapse_bvh4(all.data(), all.size(), (uint32_t)o.i0, &n4);
+        done.push_back({o.i0, r4});
+      }
+      o.i0 = (int32_t)r4;
+    }
+    if ((rc = upload(ctx, &ctx->nodes4, n4.data(), n4.size() * sizeof(Bvh4Node)))) return rc;
+    if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
+    FS_HIP(hipStreamSynchronize(ctx->stream));
+  }
+#endif
   DevScene& S = ctx->scene;
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
+  S.nodes4 = (const Bvh4Node*)ctx->nodes4.p;
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;

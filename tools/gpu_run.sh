@@ -3,7 +3,7 @@
 # under its own time limit; the first failing step ends the run.
 #
 # usage: bash tools/gpu_run.sh ROUND STEP [STEP ...]
-#   tests[:PYTEST_ARGS]          pytest -m gpu (log + parity records in gpurun_out/ROUND)
+#   tests[:KEXPR]                pytest -m gpu [-k KEXPR] (log + parity records in gpurun_out/ROUND)
 #   smoke                        __graft_entry__.smoke()
 #   bench:SCENE[:WxH[:STEPS]]    one bench.py line -> bench_SCENE_WxH.json (C4 1080p adds the CPU baseline)
 #   prof[:SCENE]                 rocprofv3 --kernel-trace --stats of the bench command -> prof_SCENE/
@@ -12,6 +12,9 @@
 #   ab:VARIANTS:SCENES:SPP:ROUNDS   tools/perf_ab.py (fs_options A/B in one process)
 #   libab:LIBS:SCENES:SPP:ROUNDS    alternating processes over in-tree builds (space-separated .so names)
 #   phase:SCENES:SPP             per-phase cycle split (needs the in-tree libfsgpu_prof.so)
+#   lib:NAME                     the steps after it load final-stage-path-tracer-2-0_amd/NAME (an A/B build)
+#                                through FSAMD_GPU_LIB; "lib:" alone returns to the product libfsgpu.so
+#   bench:SCENE:WxH:STEPS:SPP    as bench, with a shorter spp (A/B counts)
 set -o pipefail
 R=$1
 shift
@@ -24,22 +27,26 @@ for step in "$@"; do
   IFS=: read -r name a1 a2 a3 a4 <<< "$step"
   echo "== $step ($(date +%T))"
   case $name in
+    lib)
+      if [ -n "$a1" ]; then export FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/$a1; else unset FSAMD_GPU_LIB; fi
+      echo "FSAMD_GPU_LIB=${FSAMD_GPU_LIB:-}" ;;
     tests)
       rm -f gpurun_out/parity_records.jsonl
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread $a1 \
-        > $OUT/pytest_gpu.log 2>&1 || fail $step $? $OUT/pytest_gpu.log
+      log=$OUT/pytest_gpu$([ -n "${FSAMD_GPU_LIB:-}" ] && basename ${FSAMD_GPU_LIB%.so} | sed 's/^/_/').log
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${a1:+-k "$a1"} \
+        > $log 2>&1 || fail $step $? $log
       [ -f gpurun_out/parity_records.jsonl ] && mv gpurun_out/parity_records.jsonl $OUT/
-      tail -2 $OUT/pytest_gpu.log ;;
+      tail -2 $log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
         || fail $step $? $OUT/smoke.log
       tail -2 $OUT/smoke.log ;;
     bench)
-      sc=${a1:-c4}; wh=${a2:-1920x1080}; w=${wh%x*}; h=${wh#*x}; st=${a3:-3}
-      cpu=--no-cpu; [ "$sc$wh" = c41920x1080 ] && cpu=
-      f=$OUT/bench_${sc}_${wh}
-      timeout -k 10 600 python bench.py --scene $sc --width $w --height $h --steps $st $cpu > $f.json 2> $f.err \
-        || fail $step $? $f.err
+      sc=${a1:-c4}; wh=${a2:-1920x1080}; w=${wh%x*}; h=${wh#*x}; st=${a3:-3}; spp=${a4:-1024}
+      cpu=--no-cpu; [ "$sc$wh$spp" = c41920x10801024 ] && [ -z "${FSAMD_GPU_LIB:-}" ] && cpu=
+      f=$OUT/bench_${sc}_${wh}$([ "$spp" = 1024 ] || echo "_$spp")$([ -n "${FSAMD_GPU_LIB:-}" ] && basename ${FSAMD_GPU_LIB%.so} | sed 's/^/_/')
+      timeout -k 10 600 python bench.py --scene $sc --width $w --height $h --steps $st --spp $spp $cpu > $f.json \
+        2> $f.err || fail $step $? $f.err
       cut -c1-220 $f.json ;;
     prof)
       sc=${a1:-c4}
