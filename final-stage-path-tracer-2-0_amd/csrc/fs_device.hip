@@ -30,8 +30,11 @@
 // lane-major HBM shading rows, object heads as one scalar load, 12-B radiance
 // records. The only remaining switch is FS_PHASE_PROF (the profiling build,
 // libfsgpu_prof.so).
-#ifndef FS_BVH4  // round-4 A/B: walks over 4-wide nodes collapsed from the BVH2 (1)
+#ifndef FS_BVH4  // round-4 A/B: walks over 4-wide nodes collapsed from the BVH2 (1; 2: fp16 boxes)
 #define FS_BVH4 0
+#endif
+#ifndef FS_OBJ_PREFETCH  // round-4 A/B: object heads loaded one object ahead
+#define FS_OBJ_PREFETCH 0
 #endif
 
 namespace fs {
@@ -892,22 +895,47 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         // farthest first. The collapse keeps every walk's stack within
         // kTraversalStack entries, and the writes past the pushed entries
         // stay below it too (sp + pushes of this node <= the bound).
+#if FS_BVH4 == 2
+        const uint4* q = reinterpret_cast<const uint4*>(S.nodes4h + w);
+        const float4 O = reinterpret_cast<const float4*>(q)[0];
+        const uint4 PX = q[1], PY = q[2], PZ = q[3], Cw = q[4];
+        // the node origin folded into the slab constants: plane = org + h
+        const float nox = fmaf(O.x, ix, ox), noy = fmaf(O.y, iy, oy), noz = fmaf(O.z, iz, oz);
+        auto hl = [](uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xFFFFu)); };
+        auto hh = [](uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); };
+#define FS_B4_CHILD(i, H, W0, W1) H(PX.W0), H(PX.W1), H(PY.W0), H(PY.W1), H(PZ.W0), H(PZ.W1), i
+#define FS_B4_ARGS0 FS_B4_CHILD(0u, hl, x, z)
+#define FS_B4_ARGS1 FS_B4_CHILD(1u, hh, x, z)
+#define FS_B4_ARGS2 FS_B4_CHILD(2u, hl, y, w)
+#define FS_B4_ARGS3 FS_B4_CHILD(3u, hh, y, w)
+#else
         const float4* q = reinterpret_cast<const float4*>(S.nodes4 + w);
         const float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
         const uint4 Cw = reinterpret_cast<const uint4*>(q)[6];
+        const float nox = ox, noy = oy, noz = oz;
+#define FS_B4_ARGS0 LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, 0u
+#define FS_B4_ARGS1 LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, 1u
+#define FS_B4_ARGS2 LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, 2u
+#define FS_B4_ARGS3 LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, 3u
+#endif
         const int tl = __float_as_int(tmax_lim);
         auto key = [&](float lx, float hx, float ly, float hy, float lz, float hz, uint32_t i) -> uint32_t {
-          const float a = fmaf(lx, ix, ox), b = fmaf(hx, ix, ox);
-          const float c = fmaf(ly, iy, oy), e = fmaf(hy, iy, oy);
-          const float g = fmaf(lz, iz, oz), k = fmaf(hz, iz, oz);
+          const float a = fmaf(lx, ix, nox), b = fmaf(hx, ix, nox);
+          const float c = fmaf(ly, iy, noy), e = fmaf(hy, iy, noy);
+          const float g = fmaf(lz, iz, noz), k = fmaf(hz, iz, noz);
           const float n = fmaxf(fmaxf(fminf(a, b), fminf(c, e)), fmaxf(fminf(g, k), -1e-6f));
           const float f = fminf(fminf(fmaxf(a, b), fmaxf(c, e)), __int_as_float(min(__float_as_int(fmaxf(g, k)), tl)));
           return n <= f ? ((__float_as_uint(n) & 0x7FFFFFFCu) | i) : 0xFFFFFFFFu;
         };
-        uint32_t k0 = key(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, 0u);
-        uint32_t k1 = key(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, 1u);
-        uint32_t k2 = key(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, 2u);
-        uint32_t k3 = key(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, 3u);
+        uint32_t k0 = key(FS_B4_ARGS0);
+        uint32_t k1 = key(FS_B4_ARGS1);
+        uint32_t k2 = key(FS_B4_ARGS2);
+        uint32_t k3 = key(FS_B4_ARGS3);
+#undef FS_B4_ARGS0
+#undef FS_B4_ARGS1
+#undef FS_B4_ARGS2
+#undef FS_B4_ARGS3
+#undef FS_B4_CHILD
         auto cs = [](uint32_t& a, uint32_t& b) {
           const uint32_t lo = min(a, b), hi = max(a, b);
           a = lo;
@@ -1257,12 +1285,22 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
   bool park = false;
   const Slopes sl = seg_slopes(r, zl);  // once per segment: the mesh-root culls' and the walks'
+#if FS_OBJ_PREFETCH
+  ObjHead Hn;
+  if (S.num_objects) Hn = load_head(const_obj(S.objects, 0));
+#endif
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
+#if FS_OBJ_PREFETCH  // round-4 A/B: the next object's head in flight while this one is tested
+    const ObjHead H = Hn;
+    Hn = load_head(const_obj(S.objects, oi + 1 < S.num_objects ? oi + 1 : oi));
+#endif
     if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
+#if !FS_OBJ_PREFETCH
     const ObjHead H = load_head(o);
+#endif
     const float* hd = H.d;
     const int32_t kind = H.kind;
     const __attribute__((address_space(4))) float* d = o->d;
@@ -2514,7 +2552,13 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
       }
       o.i0 = (int32_t)r4;
     }
+#if FS_BVH4 == 2
+    std::vector<Bvh4HNode> n4h(n4.size());
+    for (size_t i = 0; i < n4.size(); i++) n4h[i] = compress_bvh4h(n4[i]);
+    if ((rc = upload(ctx, &ctx->nodes4, n4h.data(), n4h.size() * sizeof(Bvh4HNode)))) return rc;
+#else
     if ((rc = upload(ctx, &ctx->nodes4, n4.data(), n4.size() * sizeof(Bvh4Node)))) return rc;
+#endif
     if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
     FS_HIP(hipStreamSynchronize(ctx->stream));
   }
@@ -2523,6 +2567,7 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
   S.nodes4 = (const Bvh4Node*)ctx->nodes4.p;
+  S.nodes4h = (const Bvh4HNode*)ctx->nodes4.p;
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;

@@ -1117,6 +1117,69 @@ Cand4 child_cand(const BvhNode& nd, int c) {
 bool empty_leaf(uint32_t w) { return (w & kLeafBit) && leaf_count(w) == 0; }
 }  // namespace
 
+namespace {
+// The finite fp16 values in increasing order with their bit patterns.
+const std::vector<std::pair<double, uint16_t>>& half_table() {
+  static const std::vector<std::pair<double, uint16_t>> t = [] {
+    std::vector<std::pair<double, uint16_t>> v;
+    for (uint32_t b = 0; b < 0x10000; b++) {
+      const uint32_t e = (b >> 10) & 0x1F, m = b & 0x3FF;
+      if (e == 0x1F || b == 0x8000) continue;  // inf / NaN, and -0 (+0 stands for zero)
+      double x = e ? std::ldexp(1.0 + m / 1024.0, (int)e - 15) : std::ldexp(m / 1024.0, -14);
+      v.push_back({(b & 0x8000) ? -x : x, (uint16_t)b});
+    }
+    std::sort(v.begin(), v.end());
+    return v;
+  }();
+  return t;
+}
+// fp16 bits of the largest (down) / smallest (up) half <= / >= x, one more
+// fp16 step outward; beyond the fp16 range, -inf / +inf.
+uint16_t half_outward(double x, bool up) {
+  const auto& t = half_table();
+  if (up) {
+    auto it = std::lower_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0));
+    if (it == t.end() || it + 1 == t.end()) return 0x7C00;
+    return (it + 1)->second;
+  }
+  auto it = std::upper_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0xFFFF));
+  if (it == t.begin() || it - 1 == t.begin()) return 0xFC00;
+  return (it - 2)->second;
+}
+}  // namespace
+
+Bvh4HNode compress_bvh4h(const Bvh4Node& n) {
+  Bvh4HNode h;
+  std::memset(&h, 0, sizeof(h));
+  const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
+  const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
+  uint32_t* pk[3] = {h.px, h.py, h.pz};
+  bool used[4];
+  for (int i = 0; i < 4; i++) used[i] = n.lo_x[i] < 1e30f;
+  for (int a = 0; a < 3; a++) {
+    float o = INFINITY;
+    for (int i = 0; i < 4; i++)
+      if (used[i]) o = std::min(o, lo[a][i]);
+    if (!(o < INFINITY)) o = 0.0f;
+    h.org[a] = o;
+    uint16_t l[4], u[4];
+    for (int i = 0; i < 4; i++) {
+      if (used[i]) {
+        l[i] = half_outward((double)lo[a][i] - (double)o, false);
+        u[i] = half_outward((double)hi[a][i] - (double)o, true);
+      } else {
+        l[i] = u[i] = 0x7C00;  // +inf planes: never hit
+      }
+    }
+    pk[a][0] = l[0] | (uint32_t)l[1] << 16;
+    pk[a][1] = l[2] | (uint32_t)l[3] << 16;
+    pk[a][2] = u[0] | (uint32_t)u[1] << 16;
+    pk[a][3] = u[2] | (uint32_t)u[3] << 16;
+  }
+  for (int i = 0; i < 4; i++) h.child[i] = n.child[i];
+  return h;
+}
+
 uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out) {
   // inner-node height of every node of the tree (1: both children leaves)
   std::vector<uint8_t> height(n, 0);

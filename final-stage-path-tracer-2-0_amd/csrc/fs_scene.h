@@ -79,6 +79,21 @@ struct Bvh4Node {
   uint32_t pad[4];
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
+// BVH4 node with half-precision boxes, 80 B: the children's planes relative to
+// the node's origin (the low corner of their union), rounded outward to fp16
+// (one more fp16 step outward as a margin), packed two children per word:
+// px[0] = lo_x of children 0|1, px[1] = lo_x 2|3, px[2] = hi_x 0|1, px[3] = hi_x
+// 2|3; unused slots hold +inf planes (never hit). The walk reads them with
+// v_fma_mix_f32 (fp16 operands, fp32 arithmetic): one instruction per plane,
+// as the fp32 node, at 19 instead of 28 registers of node data.
+struct Bvh4HNode {
+  float org[3];
+  uint32_t pad;
+  uint32_t px[4], py[4], pz[4];
+  uint32_t child[4];
+};
+static_assert(sizeof(Bvh4HNode) == 80, "Bvh4HNode layout");
+Bvh4HNode compress_bvh4h(const Bvh4Node& n);
 constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces); the LDS stack bounds the waves per CU
 constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
