@@ -3029,12 +3029,65 @@ int fs_bvh_quality(const fs_scene_desc* desc, const fs_options* opt, char* out, 
         }
       }
     }
-    char buf[256];
+    // The 4-wide collapse of the same tree (collapse_bvh4, compress_bvh4h):
+    // its node count and depth, the worst-case walk stack (max over
+    // root-to-node paths of the sum of children - 1), whether its leaves are
+    // exactly the BVH2's leaf words and whether every fp16 box contains its
+    // fp32 box.
+    std::vector<Bvh4Node> n4;
+    const uint32_t r4 = collapse_bvh4(P.nodes.data(), P.nodes.size(), (uint32_t)o.i0, &n4);
+    uint64_t leaves4 = 0, faces4 = 0, not_contained = 0;
+    uint32_t depth4 = 0, stack4 = 0;
+    {
+      struct It4 {
+        uint32_t n, d, p;
+      };
+      std::vector<It4> st{{r4, 1, 0}};
+      while (!st.empty()) {
+        const It4 it = st.back();
+        st.pop_back();
+        const Bvh4Node& nd = n4[it.n];
+        const Bvh4HNode hn = compress_bvh4h(nd);
+        uint32_t k = 0;
+        for (int c = 0; c < 4; c++) k += nd.lo_x[c] < 1e30f;
+        const uint32_t p = it.p + (k ? k - 1 : 0);
+        stack4 = std::max(stack4, p);
+        depth4 = std::max(depth4, it.d);
+        const uint32_t* pk[3] = {hn.px, hn.py, hn.pz};
+        const float* lo[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
+        const float* hi[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
+        for (int c = 0; c < 4; c++) {
+          if (!(nd.lo_x[c] < 1e30f)) continue;
+          for (int a = 0; a < 3; a++) {  // the fp16 planes, decoded as the walk decodes them (org + h)
+            const uint32_t wl = pk[a][c >> 1], wh = pk[a][2 + (c >> 1)];
+            const uint16_t bl = (uint16_t)((c & 1) ? wl >> 16 : wl), bh = (uint16_t)((c & 1) ? wh >> 16 : wh);
+            auto dec = [](uint16_t b) {
+              const uint32_t e = (b >> 10) & 0x1F, m = b & 0x3FF;
+              double x = e == 0x1F ? INFINITY : e ? std::ldexp(1.0 + m / 1024.0, (int)e - 15) : std::ldexp(m / 1024.0, -14);
+              return (b & 0x8000) ? -x : x;
+            };
+            if (!((double)hn.org[a] + dec(bl) <= (double)lo[a][c] && (double)hn.org[a] + dec(bh) >= (double)hi[a][c]))
+              not_contained++;
+          }
+          const uint32_t w = nd.child[c];
+          if (w & kLeafBit) {
+            leaves4++;
+            faces4 += leaf_count(w);
+          } else {
+            st.push_back({w, it.d + 1, p});
+          }
+        }
+      }
+    }
+    char buf[512];
     std::snprintf(buf, sizeof buf,
                   "%s{\"object\": %zu, \"nodes\": %llu, \"leaves\": %llu, \"faces\": %llu, \"depth\": %u, "
+                  "\"bvh4_nodes\": %zu, \"bvh4_depth\": %u, \"bvh4_leaves\": %llu, \"bvh4_faces\": %llu, "
+                  "\"bvh4_max_stack\": %u, \"bvh4h_boxes_not_contained\": %llu, "
                   "\"sah_cost\": %.4f, \"overlap_weighted\": %.4f, \"overlap_per_level\": [",
                   js.size() > 1 ? ", " : "", oi, (unsigned long long)nodes, (unsigned long long)leaves,
-                  (unsigned long long)faces, depth, sah, ov_w);
+                  (unsigned long long)faces, depth, n4.size(), depth4, (unsigned long long)leaves4,
+                  (unsigned long long)faces4, stack4, (unsigned long long)not_contained, sah, ov_w);
     js += buf;
     for (size_t l = 0; l < ov_sum.size(); l++) {
       std::snprintf(buf, sizeof buf, "%s%.4f", l ? ", " : "", ov_n[l] ? ov_sum[l] / ov_n[l] : 0.0);
