@@ -2541,8 +2541,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
     FS_HIP(hipMemcpy(all.data(), ctx->nodes.p, all.size() * sizeof(BvhNode), hipMemcpyDeviceToHost));
     std::vector<Bvh4Node> n4;
     std::vector<std::pair<int32_t, uint32_t>> done;  // BVH2 root -> BVH4 root (meshes shared by objects)
-    for (DevObject& o : P.objects) {
-      if (o.kind != FS_OBJ_MESH || !o.i2 || o.i3) continue;
+    for (DevObject& o : P.objects) {  // small meshes too: stale_texcoords walks them
+      if (o.kind != FS_OBJ_MESH || !o.i2) continue;
       uint32_t r4 = 0xFFFFFFFFu;
       for (auto& d : done)
         if (d.first == o.i0) r4 = d.second;

@@ -21,7 +21,7 @@ shift
 OUT=gpurun_out/$R
 mkdir -p $OUT
 export TMPDIR=/tmp
-fail() { echo "step $1 failed (rc $2)"; [ -n "$3" ] && tail -25 "$3"; exit 1; }
+fail() { echo "step failed (rc $2): $1"; [ -n "$3" ] && tail -25 "$3"; exit 1; }
 
 for step in "$@"; do
   IFS=: read -r name a1 a2 a3 a4 <<< "$step"
@@ -34,25 +34,25 @@ for step in "$@"; do
       rm -f gpurun_out/parity_records.jsonl
       log=$OUT/pytest_gpu$([ -n "${FSAMD_GPU_LIB:-}" ] && basename ${FSAMD_GPU_LIB%.so} | sed 's/^/_/').log
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ${a1:+-k "$a1"} \
-        > $log 2>&1 || fail $step $? $log
+        > $log 2>&1 || fail "$step" $? $log
       [ -f gpurun_out/parity_records.jsonl ] && mv gpurun_out/parity_records.jsonl $OUT/
       tail -2 $log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
-        || fail $step $? $OUT/smoke.log
+        || fail "$step" $? $OUT/smoke.log
       tail -2 $OUT/smoke.log ;;
     bench)
       sc=${a1:-c4}; wh=${a2:-1920x1080}; w=${wh%x*}; h=${wh#*x}; st=${a3:-3}; spp=${a4:-1024}
       cpu=--no-cpu; [ "$sc$wh$spp" = c41920x10801024 ] && [ -z "${FSAMD_GPU_LIB:-}" ] && cpu=
       f=$OUT/bench_${sc}_${wh}$([ "$spp" = 1024 ] || echo "_$spp")$([ -n "${FSAMD_GPU_LIB:-}" ] && basename ${FSAMD_GPU_LIB%.so} | sed 's/^/_/')
       timeout -k 10 600 python bench.py --scene $sc --width $w --height $h --steps $st --spp $spp $cpu > $f.json \
-        2> $f.err || fail $step $? $f.err
+        2> $f.err || fail "$step" $? $f.err
       cut -c1-220 $f.json ;;
     prof)
       sc=${a1:-c4}
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$sc -o trace -- \
         python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu > $OUT/prof_$sc.json 2> $OUT/prof_$sc.err \
-        || fail $step $? $OUT/prof_$sc.err
+        || fail "$step" $? $OUT/prof_$sc.err
       find $OUT/prof_$sc -name "*kernel_stats.csv" -exec cut -c1-160 {} \; ;;
     pmc)
       sc=$a1; wh=$a2; w=${wh%x*}; h=${wh#*x}; spp=$a3
@@ -69,13 +69,13 @@ for step in "$@"; do
           > $d/p$i.out 2> $d/p$i.err || fail "$step pass $i" $? $d/p$i.err
       done
       kern=$(python3 -c "import json; print([json.loads(l) for l in open('$d/p1.out') if l.startswith('{')][-1]['roofline']['kernel'])") \
-        || fail $step $?
+        || fail "$step" $?
       python3 tools/pmc_summary.py $d "$kern" $OUT/pmc_${sc}_${wh}.json "$sc ${wh} x $spp spp, one launch" \
-        $((w * h * spp)) > $d/summary.log 2>&1 || fail $step $? $d/summary.log
+        $((w * h * spp)) > $d/summary.log 2>&1 || fail "$step" $? $d/summary.log
       grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $OUT/pmc_${sc}_${wh}.json ;;
     ab)
       log=$OUT/ab_$(date +%H%M%S).log
-      timeout -k 10 900 python tools/perf_ab.py "$a1" "$a2" ${a3:-256} ${a4:-2} > $log 2>&1 || fail $step $? $log
+      timeout -k 10 900 python tools/perf_ab.py "$a1" "$a2" ${a3:-256} ${a4:-2} > $log 2>&1 || fail "$step" $? $log
       grep -E "variant|differs|md5" $log ;;
     libab)
       log=$OUT/libab_$(date +%H%M%S).log
@@ -83,13 +83,13 @@ for step in "$@"; do
         for L in $a1; do
           echo "== $L" >> $log
           FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/$L timeout -k 10 300 \
-            python tools/perf_ab.py default "$a2" ${a3:-256} 1 >> $log 2>&1 || fail $step $? $log
+            python tools/perf_ab.py default "$a2" ${a3:-256} 1 >> $log 2>&1 || fail "$step" $? $log
         done
       done
       grep -E "^==|variant" $log ;;
     phase)
       FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/libfsgpu_prof.so timeout -k 10 600 \
-        python tools/phase_prof.py "$a1" ${a2:-64} > $OUT/phase.log 2>&1 || fail $step $? $OUT/phase.log
+        python tools/phase_prof.py "$a1" ${a2:-64} > $OUT/phase.log 2>&1 || fail "$step" $? $OUT/phase.log
       grep -E "==|phase|trips" $OUT/phase.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
