@@ -895,8 +895,15 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         // farthest first. The collapse keeps every walk's stack within
         // kTraversalStack entries, and the writes past the pushed entries
         // stay below it too (sp + pushes of this node <= the bound).
-#if FS_BVH4 == 2
-        const uint4* q = reinterpret_cast<const uint4*>(S.nodes4h + w);
+#if FS_BVH4 >= 2
+#if FS_BVH4 == 3
+        // a revisit entry: the node again, without the children in its mask
+        const uint32_t excl = (w >> 27) & 15u;
+        const uint32_t node = w & 0x07FFFFFFu;
+#else
+        const uint32_t node = w;
+#endif
+        const uint4* q = reinterpret_cast<const uint4*>(S.nodes4h + node);
         const float4 O = reinterpret_cast<const float4*>(q)[0];
         const uint4 PX = q[1], PY = q[2], PZ = q[3], Cw = q[4];
         // the node origin folded into the slab constants: plane = org + h
@@ -931,6 +938,12 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         uint32_t k1 = key(FS_B4_ARGS1);
         uint32_t k2 = key(FS_B4_ARGS2);
         uint32_t k3 = key(FS_B4_ARGS3);
+#if FS_BVH4 == 3
+        k0 = (excl & 1u) ? 0xFFFFFFFFu : k0;
+        k1 = (excl & 2u) ? 0xFFFFFFFFu : k1;
+        k2 = (excl & 4u) ? 0xFFFFFFFFu : k2;
+        k3 = (excl & 8u) ? 0xFFFFFFFFu : k3;
+#endif
 #undef FS_B4_ARGS0
 #undef FS_B4_ARGS1
 #undef FS_B4_ARGS2
@@ -952,13 +965,30 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         if (k0 == 0xFFFFFFFFu) {
           w = sp ? stk[--sp * kBlock] : kNone;
         } else {
-          w = sel(k0);
-          stk[sp * kBlock] = sel(k3);
-          sp += k3 != 0xFFFFFFFFu;
-          stk[sp * kBlock] = sel(k2);
-          sp += k2 != 0xFFFFFFFFu;
-          stk[sp * kBlock] = sel(k1);
-          sp += k1 != 0xFFFFFFFFu;
+#if FS_BVH4 == 3
+          // Pushes only while the stack keeps room for one entry per level
+          // below (R, from the node); otherwise one revisit entry stands for
+          // all the children not yet taken. It pops after the nearest child's
+          // subtree is done, and the node's test runs again without the
+          // children in its mask (culling with a t limit that can only have
+          // shrunk is still conservative), so the walk tests the same
+          // triangles and its closest hit is unchanged.
+          const uint32_t npush = (k1 != 0xFFFFFFFFu) + (k2 != 0xFFFFFFFFu) + (k3 != 0xFFFFFFFFu);
+          if (sp + npush + __float_as_uint(O.w) > kTraversalStack) {
+            stk[sp * kBlock] = node | ((excl | 1u << (k0 & 3u)) << 27);
+            sp += npush != 0;
+            w = sel(k0);
+          } else
+#endif
+          {
+            w = sel(k0);
+            stk[sp * kBlock] = sel(k3);
+            sp += k3 != 0xFFFFFFFFu;
+            stk[sp * kBlock] = sel(k2);
+            sp += k2 != 0xFFFFFFFFu;
+            stk[sp * kBlock] = sel(k1);
+            sp += k1 != 0xFFFFFFFFu;
+          }
         }
       }
 #else
@@ -2547,12 +2577,15 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
       for (auto& d : done)
         if (d.first == o.i0) r4 = d.second;
       if (r4 == 0xFFFFFFFFu) {
-        r4 = collapse_bvh4(all.data(), all.size(), (uint32_t)o.i0, &n4);
+        r4 = collapse_bvh4(all.data(), all.size(), (uint32_t)o.i0, &n4, FS_BVH4 == 3);
         done.push_back({o.i0, r4});
       }
       o.i0 = (int32_t)r4;
     }
-#if FS_BVH4 == 2
+#if FS_BVH4 == 3
+    if (n4.size() >= (1u << 27)) return fail(FS_ERR_INVALID, "more than 2^27 BVH4 nodes");
+#endif
+#if FS_BVH4 >= 2
     std::vector<Bvh4HNode> n4h(n4.size());
     for (size_t i = 0; i < n4.size(); i++) n4h[i] = compress_bvh4h(n4[i]);
     if ((rc = upload(ctx, &ctx->nodes4, n4h.data(), n4h.size() * sizeof(Bvh4HNode)))) return rc;
@@ -3079,15 +3112,20 @@ int fs_bvh_quality(const fs_scene_desc* desc, const fs_options* opt, char* out, 
         }
       }
     }
-    char buf[512];
+    // the unbudgeted collapse (revisit entries bound the stack at run time)
+    std::vector<Bvh4Node> nf;
+    const uint32_t rf = collapse_bvh4(P.nodes.data(), P.nodes.size(), (uint32_t)o.i0, &nf, true);
+    char buf[640];
     std::snprintf(buf, sizeof buf,
                   "%s{\"object\": %zu, \"nodes\": %llu, \"leaves\": %llu, \"faces\": %llu, \"depth\": %u, "
                   "\"bvh4_nodes\": %zu, \"bvh4_depth\": %u, \"bvh4_leaves\": %llu, \"bvh4_faces\": %llu, "
                   "\"bvh4_max_stack\": %u, \"bvh4h_boxes_not_contained\": %llu, "
+                  "\"bvh4full_nodes\": %zu, \"bvh4full_height\": %u, "
                   "\"sah_cost\": %.4f, \"overlap_weighted\": %.4f, \"overlap_per_level\": [",
                   js.size() > 1 ? ", " : "", oi, (unsigned long long)nodes, (unsigned long long)leaves,
                   (unsigned long long)faces, depth, n4.size(), depth4, (unsigned long long)leaves4,
-                  (unsigned long long)faces4, stack4, (unsigned long long)not_contained, sah, ov_w);
+                  (unsigned long long)faces4, stack4, (unsigned long long)not_contained, nf.size(), nf[rf].pad[0] + 1,
+                  sah, ov_w);
     js += buf;
     for (size_t l = 0; l < ov_sum.size(); l++) {
       std::snprintf(buf, sizeof buf, "%s%.4f", l ? ", " : "", ov_n[l] ? ov_sum[l] / ov_n[l] : 0.0);

@@ -1177,10 +1177,11 @@ Bvh4HNode compress_bvh4h(const Bvh4Node& n) {
     pk[a][3] = u[2] | (uint32_t)u[3] << 16;
   }
   for (int i = 0; i < 4; i++) h.child[i] = n.child[i];
+  h.pad = n.pad[0];
   return h;
 }
 
-uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out) {
+uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out, bool full) {
   // inner-node height of every node of the tree (1: both children leaves)
   std::vector<uint8_t> height(n, 0);
   {
@@ -1216,6 +1217,7 @@ uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vecto
       if (!empty_leaf(nodes[jb.v2].child[c])) cs.push_back(child_cand(nodes[jb.v2], c));
     // every inner child's subtree, walked as the binary tree below it, must fit
     auto fits = [&](const std::vector<Cand4>& set) {
+      if (full) return true;
       const uint32_t p = jb.pushes + (uint32_t)set.size() - 1;
       if (p > kTraversalStack) return false;
       for (const Cand4& k : set)
@@ -1259,6 +1261,14 @@ uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vecto
       }
     }
     (*out)[jb.slot4] = nd;
+  }
+  // R per node (pad[0]): children before parents in reverse creation order
+  for (size_t i = out->size(); i-- > root4;) {
+    Bvh4Node& nd = (*out)[i];
+    uint32_t r = 0;
+    for (int c = 0; c < 4; c++)
+      if (!(nd.child[c] & kLeafBit)) r = std::max(r, 1 + (*out)[nd.child[c]].pad[0]);
+    nd.pad[0] = r;
   }
   return root4;
 }

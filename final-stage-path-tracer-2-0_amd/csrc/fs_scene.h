@@ -188,7 +188,12 @@ struct BuildOptions {
 // the un-popped siblings of its ancestors, so along every root-to-node path
 // the sum of (children - 1) must fit, counting the binary BVH2 height of the
 // subtrees below. The leaves (triangle slots) are the BVH2's.
-uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out);
+// full: no stack budget (every node takes up to four children); the walk
+// then bounds its stack at run time with revisit entries (fs_device.hip), and
+// each node's pad[0] holds R, the stack entries a walk below it may need
+// when every node pushes one entry (the BVH4 height below it).
+uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out,
+                       bool full = false);
 
 // Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
 // one SAH BVH per mesh. Returns FS_OK or an fs_status with *err set.
