@@ -33,6 +33,9 @@
 #ifndef FS_BVH4  // round-4 A/B: walks over 4-wide nodes collapsed from the BVH2 (1; 2: fp16 boxes)
 #define FS_BVH4 0
 #endif
+#ifndef FS_FACES_FIRST  // round-4 A/B: meshes of at most this many faces test them before the root cull
+#define FS_FACES_FIRST 0
+#endif
 #ifndef FS_OBJ_PREFETCH  // round-4 A/B: object heads loaded one object ahead
 #define FS_OBJ_PREFETCH 0
 #endif
@@ -1338,6 +1341,23 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       if (!H.i2) continue;
       uint64_t t0 = FS_TICK();
       const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
+#if FS_FACES_FIRST
+      // round-4 A/B: a mesh of at most FS_FACES_FIRST faces tests its faces
+      // first and runs the root cull only in lanes whose hit its faces
+      // improved (with the best t from before the mesh): the reference's
+      // cull only matters where the mesh would change the hit, so a lane the
+      // cull rejects gets its previous hit back. Exact, and a quad (two
+      // faces, one plane test) costs less than its cull.
+      if (H.i3 && (uint32_t)H.i3 <= FS_FACES_FIRST) {
+        const MinHit h0 = h;
+        small_mesh_trace<COUNT>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
+        if (h.obj == (int32_t)oi &&
+            !ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h0.t, sl))
+          h = h0;
+        if (TEX && h.obj == (int32_t)oi && H.i4) h.tc = (int32_t)oi;
+        continue;
+      }
+#endif
       bool visit =
           resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t, sl);
       uint64_t t1 = FS_TICK();
