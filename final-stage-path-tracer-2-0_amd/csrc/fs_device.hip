@@ -30,15 +30,6 @@
 // lane-major HBM shading rows, object heads as one scalar load, 12-B radiance
 // records. The only remaining switch is FS_PHASE_PROF (the profiling build,
 // libfsgpu_prof.so).
-#ifndef FS_BVH4  // round-4 A/B: walks over 4-wide nodes collapsed from the BVH2 (1; 2: fp16 boxes)
-#define FS_BVH4 0
-#endif
-#ifndef FS_FACES_FIRST  // round-4 A/B: meshes of at most this many faces test them before the root cull
-#define FS_FACES_FIRST 0
-#endif
-#ifndef FS_OBJ_PREFETCH  // round-4 A/B: object heads loaded one object ahead
-#define FS_OBJ_PREFETCH 0
-#endif
 
 namespace fs {
 namespace dev {
@@ -885,119 +876,14 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   bool susp = false;
   while ((w != kNone || leaf) && !(SUSP && susp)) {
     while (!(w & kLeafBit) && w != kNone) {
+      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
+      float4 X = q[0], Y = q[1], Z = q[2];
+      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       if (COUNT) tally.nodes++;
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.node_trips);
       tally.lane_nodes++;
 #endif
-#if FS_BVH4
-      {
-        // Four child boxes per trip. Hit children get keys (entry time bits,
-        // child index in the low 2 bits; a miss 0xFFFFFFFF), sorted by a
-        // 5-comparator network: the nearest goes on, the others are pushed
-        // farthest first. The collapse keeps every walk's stack within
-        // kTraversalStack entries, and the writes past the pushed entries
-        // stay below it too (sp + pushes of this node <= the bound).
-#if FS_BVH4 >= 2
-#if FS_BVH4 == 3
-        // a revisit entry: the node again, without the children in its mask
-        const uint32_t excl = (w >> 27) & 15u;
-        const uint32_t node = w & 0x07FFFFFFu;
-#else
-        const uint32_t node = w;
-#endif
-        const uint4* q = reinterpret_cast<const uint4*>(S.nodes4h + node);
-        const float4 O = reinterpret_cast<const float4*>(q)[0];
-        const uint4 PX = q[1], PY = q[2], PZ = q[3], Cw = q[4];
-        // the node origin folded into the slab constants: plane = org + h
-        const float nox = fmaf(O.x, ix, ox), noy = fmaf(O.y, iy, oy), noz = fmaf(O.z, iz, oz);
-        auto hl = [](uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xFFFFu)); };
-        auto hh = [](uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); };
-#define FS_B4_CHILD(i, H, W0, W1) H(PX.W0), H(PX.W1), H(PY.W0), H(PY.W1), H(PZ.W0), H(PZ.W1), i
-#define FS_B4_ARGS0 FS_B4_CHILD(0u, hl, x, z)
-#define FS_B4_ARGS1 FS_B4_CHILD(1u, hh, x, z)
-#define FS_B4_ARGS2 FS_B4_CHILD(2u, hl, y, w)
-#define FS_B4_ARGS3 FS_B4_CHILD(3u, hh, y, w)
-#else
-        const float4* q = reinterpret_cast<const float4*>(S.nodes4 + w);
-        const float4 LX = q[0], HX = q[1], LY = q[2], HY = q[3], LZ = q[4], HZ = q[5];
-        const uint4 Cw = reinterpret_cast<const uint4*>(q)[6];
-        const float nox = ox, noy = oy, noz = oz;
-#define FS_B4_ARGS0 LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, 0u
-#define FS_B4_ARGS1 LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, 1u
-#define FS_B4_ARGS2 LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, 2u
-#define FS_B4_ARGS3 LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, 3u
-#endif
-        const int tl = __float_as_int(tmax_lim);
-        auto key = [&](float lx, float hx, float ly, float hy, float lz, float hz, uint32_t i) -> uint32_t {
-          const float a = fmaf(lx, ix, nox), b = fmaf(hx, ix, nox);
-          const float c = fmaf(ly, iy, noy), e = fmaf(hy, iy, noy);
-          const float g = fmaf(lz, iz, noz), k = fmaf(hz, iz, noz);
-          const float n = fmaxf(fmaxf(fminf(a, b), fminf(c, e)), fmaxf(fminf(g, k), -1e-6f));
-          const float f = fminf(fminf(fmaxf(a, b), fmaxf(c, e)), __int_as_float(min(__float_as_int(fmaxf(g, k)), tl)));
-          return n <= f ? ((__float_as_uint(n) & 0x7FFFFFFCu) | i) : 0xFFFFFFFFu;
-        };
-        uint32_t k0 = key(FS_B4_ARGS0);
-        uint32_t k1 = key(FS_B4_ARGS1);
-        uint32_t k2 = key(FS_B4_ARGS2);
-        uint32_t k3 = key(FS_B4_ARGS3);
-#if FS_BVH4 == 3
-        k0 = (excl & 1u) ? 0xFFFFFFFFu : k0;
-        k1 = (excl & 2u) ? 0xFFFFFFFFu : k1;
-        k2 = (excl & 4u) ? 0xFFFFFFFFu : k2;
-        k3 = (excl & 8u) ? 0xFFFFFFFFu : k3;
-#endif
-#undef FS_B4_ARGS0
-#undef FS_B4_ARGS1
-#undef FS_B4_ARGS2
-#undef FS_B4_ARGS3
-#undef FS_B4_CHILD
-        auto cs = [](uint32_t& a, uint32_t& b) {
-          const uint32_t lo = min(a, b), hi = max(a, b);
-          a = lo;
-          b = hi;
-        };
-        cs(k0, k1);
-        cs(k2, k3);
-        cs(k0, k2);
-        cs(k1, k3);
-        cs(k1, k2);
-        auto sel = [&](uint32_t k) {
-          return (k & 2u) ? ((k & 1u) ? Cw.w : Cw.z) : ((k & 1u) ? Cw.y : Cw.x);
-        };
-        if (k0 == 0xFFFFFFFFu) {
-          w = sp ? stk[--sp * kBlock] : kNone;
-        } else {
-#if FS_BVH4 == 3
-          // Pushes only while the stack keeps room for one entry per level
-          // below (R, from the node); otherwise one revisit entry stands for
-          // all the children not yet taken. It pops after the nearest child's
-          // subtree is done, and the node's test runs again without the
-          // children in its mask (culling with a t limit that can only have
-          // shrunk is still conservative), so the walk tests the same
-          // triangles and its closest hit is unchanged.
-          const uint32_t npush = (k1 != 0xFFFFFFFFu) + (k2 != 0xFFFFFFFFu) + (k3 != 0xFFFFFFFFu);
-          if (sp + npush + __float_as_uint(O.w) > kTraversalStack) {
-            stk[sp * kBlock] = node | ((excl | 1u << (k0 & 3u)) << 27);
-            sp += npush != 0;
-            w = sel(k0);
-          } else
-#endif
-          {
-            w = sel(k0);
-            stk[sp * kBlock] = sel(k3);
-            sp += k3 != 0xFFFFFFFFu;
-            stk[sp * kBlock] = sel(k2);
-            sp += k2 != 0xFFFFFFFFu;
-            stk[sp * kBlock] = sel(k1);
-            sp += k1 != 0xFFFFFFFFu;
-          }
-        }
-      }
-#else
-      const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
-      float4 X = q[0], Y = q[1], Z = q[2];
-      uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
       bool h0, h1;
       float t0, t1;
       {
@@ -1031,7 +917,6 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       } else {
         w = sp ? stk[--sp * kBlock] : kNone;
       }
-#endif
       if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
         leaf = w;
         w = sp ? stk[--sp * kBlock] : kNone;
@@ -1318,22 +1203,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
   bool park = false;
   const Slopes sl = seg_slopes(r, zl);  // once per segment: the mesh-root culls' and the walks'
-#if FS_OBJ_PREFETCH
-  ObjHead Hn;
-  if (S.num_objects) Hn = load_head(const_obj(S.objects, 0));
-#endif
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
-#if FS_OBJ_PREFETCH  // round-4 A/B: the next object's head in flight while this one is tested
-    const ObjHead H = Hn;
-    Hn = load_head(const_obj(S.objects, oi + 1 < S.num_objects ? oi + 1 : oi));
-#endif
     if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
     ConstObj o = const_obj(S.objects, oi);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.objs++;
-#if !FS_OBJ_PREFETCH
     const ObjHead H = load_head(o);
-#endif
     const float* hd = H.d;
     const int32_t kind = H.kind;
     const __attribute__((address_space(4))) float* d = o->d;
@@ -1341,23 +1216,6 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       if (!H.i2) continue;
       uint64_t t0 = FS_TICK();
       const bool resume_here = SUSP && resuming && (uint32_t)ws->oi == oi;
-#if FS_FACES_FIRST
-      // round-4 A/B: a mesh of at most FS_FACES_FIRST faces tests its faces
-      // first and runs the root cull only in lanes whose hit its faces
-      // improved (with the best t from before the mesh): the reference's
-      // cull only matters where the mesh would change the hit, so a lane the
-      // cull rejects gets its previous hit back. Exact, and a quad (two
-      // faces, one plane test) costs less than its cull.
-      if (H.i3 && (uint32_t)H.i3 <= FS_FACES_FIRST) {
-        const MinHit h0 = h;
-        small_mesh_trace<COUNT>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
-        if (h.obj == (int32_t)oi &&
-            !ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h0.t, sl))
-          h = h0;
-        if (TEX && h.obj == (int32_t)oi && H.i4) h.tc = (int32_t)oi;
-        continue;
-      }
-#endif
       bool visit =
           resume_here || ref_root_visit(mk3(hd[0], hd[1], hd[2]), mk3(hd[3], hd[4], hd[5]), r, zl, h.t, sl);
       uint64_t t1 = FS_TICK();
@@ -2178,7 +2036,7 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, nodes4, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
+  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
       pack_recv, range_io, tree, tree_objs;
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
@@ -2468,7 +2326,7 @@ int fs_destroy(fs_context* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->nodes4, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
+  for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
@@ -2585,42 +2443,9 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
                    D.num_tris, res.build_ms, res.levels, res.nodes_used, res.max_depth);
     D = DeferredMesh();  // release the host copies
   }
-#if FS_BVH4
-  {  // every walked mesh's BVH2 collapsed into 4-wide nodes (host; the device-built trees come back first)
-    std::vector<BvhNode> all(ctx->nodes.bytes / sizeof(BvhNode));
-    FS_HIP(hipMemcpy(all.data(), ctx->nodes.p, all.size() * sizeof(BvhNode), hipMemcpyDeviceToHost));
-    std::vector<Bvh4Node> n4;
-    std::vector<std::pair<int32_t, uint32_t>> done;  // BVH2 root -> BVH4 root (meshes shared by objects)
-    for (DevObject& o : P.objects) {  // small meshes too: stale_texcoords walks them
-      if (o.kind != FS_OBJ_MESH || !o.i2) continue;
-      uint32_t r4 = 0xFFFFFFFFu;
-      for (auto& d : done)
-        if (d.first == o.i0) r4 = d.second;
-      if (r4 == 0xFFFFFFFFu) {
-        r4 = collapse_bvh4(all.data(), all.size(), (uint32_t)o.i0, &n4, FS_BVH4 == 3);
-        done.push_back({o.i0, r4});
-      }
-      o.i0 = (int32_t)r4;
-    }
-#if FS_BVH4 == 3
-    if (n4.size() >= (1u << 27)) return fail(FS_ERR_INVALID, "more than 2^27 BVH4 nodes");
-#endif
-#if FS_BVH4 >= 2
-    std::vector<Bvh4HNode> n4h(n4.size());
-    for (size_t i = 0; i < n4.size(); i++) n4h[i] = compress_bvh4h(n4[i]);
-    if ((rc = upload(ctx, &ctx->nodes4, n4h.data(), n4h.size() * sizeof(Bvh4HNode)))) return rc;
-#else
-    if ((rc = upload(ctx, &ctx->nodes4, n4.data(), n4.size() * sizeof(Bvh4Node)))) return rc;
-#endif
-    if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
-    FS_HIP(hipStreamSynchronize(ctx->stream));
-  }
-#endif
   DevScene& S = ctx->scene;
   S.objects = (const DevObject*)ctx->objects.p;
   S.nodes = (const BvhNode*)ctx->nodes.p;
-  S.nodes4 = (const Bvh4Node*)ctx->nodes4.p;
-  S.nodes4h = (const Bvh4HNode*)ctx->nodes4.p;
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
@@ -3082,70 +2907,12 @@ int fs_bvh_quality(const fs_scene_desc* desc, const fs_options* opt, char* out, 
         }
       }
     }
-    // The 4-wide collapse of the same tree (collapse_bvh4, compress_bvh4h):
-    // its node count and depth, the worst-case walk stack (max over
-    // root-to-node paths of the sum of children - 1), whether its leaves are
-    // exactly the BVH2's leaf words and whether every fp16 box contains its
-    // fp32 box.
-    std::vector<Bvh4Node> n4;
-    const uint32_t r4 = collapse_bvh4(P.nodes.data(), P.nodes.size(), (uint32_t)o.i0, &n4);
-    uint64_t leaves4 = 0, faces4 = 0, not_contained = 0;
-    uint32_t depth4 = 0, stack4 = 0;
-    {
-      struct It4 {
-        uint32_t n, d, p;
-      };
-      std::vector<It4> st{{r4, 1, 0}};
-      while (!st.empty()) {
-        const It4 it = st.back();
-        st.pop_back();
-        const Bvh4Node& nd = n4[it.n];
-        const Bvh4HNode hn = compress_bvh4h(nd);
-        uint32_t k = 0;
-        for (int c = 0; c < 4; c++) k += nd.lo_x[c] < 1e30f;
-        const uint32_t p = it.p + (k ? k - 1 : 0);
-        stack4 = std::max(stack4, p);
-        depth4 = std::max(depth4, it.d);
-        const uint32_t* pk[3] = {hn.px, hn.py, hn.pz};
-        const float* lo[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
-        const float* hi[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
-        for (int c = 0; c < 4; c++) {
-          if (!(nd.lo_x[c] < 1e30f)) continue;
-          for (int a = 0; a < 3; a++) {  // the fp16 planes, decoded as the walk decodes them (org + h)
-            const uint32_t wl = pk[a][c >> 1], wh = pk[a][2 + (c >> 1)];
-            const uint16_t bl = (uint16_t)((c & 1) ? wl >> 16 : wl), bh = (uint16_t)((c & 1) ? wh >> 16 : wh);
-            auto dec = [](uint16_t b) {
-              const uint32_t e = (b >> 10) & 0x1F, m = b & 0x3FF;
-              double x = e == 0x1F ? INFINITY : e ? std::ldexp(1.0 + m / 1024.0, (int)e - 15) : std::ldexp(m / 1024.0, -14);
-              return (b & 0x8000) ? -x : x;
-            };
-            if (!((double)hn.org[a] + dec(bl) <= (double)lo[a][c] && (double)hn.org[a] + dec(bh) >= (double)hi[a][c]))
-              not_contained++;
-          }
-          const uint32_t w = nd.child[c];
-          if (w & kLeafBit) {
-            leaves4++;
-            faces4 += leaf_count(w);
-          } else {
-            st.push_back({w, it.d + 1, p});
-          }
-        }
-      }
-    }
-    // the unbudgeted collapse (revisit entries bound the stack at run time)
-    std::vector<Bvh4Node> nf;
-    const uint32_t rf = collapse_bvh4(P.nodes.data(), P.nodes.size(), (uint32_t)o.i0, &nf, true);
-    char buf[640];
+    char buf[256];
     std::snprintf(buf, sizeof buf,
                   "%s{\"object\": %zu, \"nodes\": %llu, \"leaves\": %llu, \"faces\": %llu, \"depth\": %u, "
-                  "\"bvh4_nodes\": %zu, \"bvh4_depth\": %u, \"bvh4_leaves\": %llu, \"bvh4_faces\": %llu, "
-                  "\"bvh4_max_stack\": %u, \"bvh4h_boxes_not_contained\": %llu, "
-                  "\"bvh4full_nodes\": %zu, \"bvh4full_height\": %u, "
                   "\"sah_cost\": %.4f, \"overlap_weighted\": %.4f, \"overlap_per_level\": [",
                   js.size() > 1 ? ", " : "", oi, (unsigned long long)nodes, (unsigned long long)leaves,
-                  (unsigned long long)faces, depth, n4.size(), depth4, (unsigned long long)leaves4,
-                  (unsigned long long)faces4, stack4, (unsigned long long)not_contained, nf.size(), nf[rf].pad[0] + 1,
-                  sah, ov_w);
+                  (unsigned long long)faces, depth, sah, ov_w);
     js += buf;
     for (size_t l = 0; l < ov_sum.size(); l++) {
       std::snprintf(buf, sizeof buf, "%s%.4f", l ? ", " : "", ov_n[l] ? ov_sum[l] / ov_n[l] : 0.0);

@@ -35,8 +35,6 @@ constexpr uint64_t kRadianceRowBytes = 32ull << 30;
 struct DevScene {
   const DevObject* __restrict__ objects;
   const BvhNode* __restrict__ nodes;
-  const Bvh4Node* __restrict__ nodes4;    // FS_BVH4 1 builds: the collapsed trees the walks use
-  const Bvh4HNode* __restrict__ nodes4h;  // FS_BVH4 2 builds: the same with fp16 boxes
   const DevTri* __restrict__ tris;
   const float4* __restrict__ tri_normals;
   const fs_material* __restrict__ materials;

@@ -1094,183 +1094,4 @@ int prepare_scene(const fs_scene_desc* d, PreparedScene* out, std::string* err, 
   return FS_OK;
 }
 
-namespace {
-struct Cand4 {
-  uint32_t word;  // inner BVH2 node index or leaf word
-  float lo[3], hi[3];
-  double area;
-};
-Cand4 child_cand(const BvhNode& nd, int c) {
-  Cand4 k;
-  k.word = nd.child[c];
-  k.lo[0] = nd.lo_x[c];
-  k.lo[1] = nd.lo_y[c];
-  k.lo[2] = nd.lo_z[c];
-  k.hi[0] = nd.hi_x[c];
-  k.hi[1] = nd.hi_y[c];
-  k.hi[2] = nd.hi_z[c];
-  const double dx = std::max(0.0f, k.hi[0] - k.lo[0]), dy = std::max(0.0f, k.hi[1] - k.lo[1]),
-               dz = std::max(0.0f, k.hi[2] - k.lo[2]);
-  k.area = dx * dy + dy * dz + dz * dx;
-  return k;
-}
-bool empty_leaf(uint32_t w) { return (w & kLeafBit) && leaf_count(w) == 0; }
-}  // namespace
-
-namespace {
-// The finite fp16 values in increasing order with their bit patterns.
-const std::vector<std::pair<double, uint16_t>>& half_table() {
-  static const std::vector<std::pair<double, uint16_t>> t = [] {
-    std::vector<std::pair<double, uint16_t>> v;
-    for (uint32_t b = 0; b < 0x10000; b++) {
-      const uint32_t e = (b >> 10) & 0x1F, m = b & 0x3FF;
-      if (e == 0x1F || b == 0x8000) continue;  // inf / NaN, and -0 (+0 stands for zero)
-      double x = e ? std::ldexp(1.0 + m / 1024.0, (int)e - 15) : std::ldexp(m / 1024.0, -14);
-      v.push_back({(b & 0x8000) ? -x : x, (uint16_t)b});
-    }
-    std::sort(v.begin(), v.end());
-    return v;
-  }();
-  return t;
-}
-// fp16 bits of the largest (down) / smallest (up) half <= / >= x, one more
-// fp16 step outward; beyond the fp16 range, -inf / +inf.
-uint16_t half_outward(double x, bool up) {
-  const auto& t = half_table();
-  if (up) {
-    auto it = std::lower_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0));
-    if (it == t.end() || it + 1 == t.end()) return 0x7C00;
-    return (it + 1)->second;
-  }
-  auto it = std::upper_bound(t.begin(), t.end(), std::make_pair(x, (uint16_t)0xFFFF));
-  if (it == t.begin() || it - 1 == t.begin()) return 0xFC00;
-  return (it - 2)->second;
-}
-}  // namespace
-
-Bvh4HNode compress_bvh4h(const Bvh4Node& n) {
-  Bvh4HNode h;
-  std::memset(&h, 0, sizeof(h));
-  const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
-  const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
-  uint32_t* pk[3] = {h.px, h.py, h.pz};
-  bool used[4];
-  for (int i = 0; i < 4; i++) used[i] = n.lo_x[i] < 1e30f;
-  for (int a = 0; a < 3; a++) {
-    float o = INFINITY;
-    for (int i = 0; i < 4; i++)
-      if (used[i]) o = std::min(o, lo[a][i]);
-    if (!(o < INFINITY)) o = 0.0f;
-    h.org[a] = o;
-    uint16_t l[4], u[4];
-    for (int i = 0; i < 4; i++) {
-      if (used[i]) {
-        l[i] = half_outward((double)lo[a][i] - (double)o, false);
-        u[i] = half_outward((double)hi[a][i] - (double)o, true);
-      } else {
-        l[i] = u[i] = 0x7C00;  // +inf planes: never hit
-      }
-    }
-    pk[a][0] = l[0] | (uint32_t)l[1] << 16;
-    pk[a][1] = l[2] | (uint32_t)l[3] << 16;
-    pk[a][2] = u[0] | (uint32_t)u[1] << 16;
-    pk[a][3] = u[2] | (uint32_t)u[3] << 16;
-  }
-  for (int i = 0; i < 4; i++) h.child[i] = n.child[i];
-  h.pad = n.pad[0];
-  return h;
-}
-
-uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out, bool full) {
-  // inner-node height of every node of the tree (1: both children leaves)
-  std::vector<uint8_t> height(n, 0);
-  {
-    std::vector<std::pair<uint32_t, bool>> st{{root, false}};
-    while (!st.empty()) {
-      auto [v, done] = st.back();
-      st.pop_back();
-      const BvhNode& nd = nodes[v];
-      if (done) {
-        uint8_t h = 0;
-        for (int c = 0; c < 2; c++)
-          if (!(nd.child[c] & kLeafBit)) h = std::max(h, height[nd.child[c]]);
-        height[v] = (uint8_t)(h + 1);
-        continue;
-      }
-      st.push_back({v, true});
-      for (int c = 0; c < 2; c++)
-        if (!(nd.child[c] & kLeafBit)) st.push_back({nd.child[c], false});
-    }
-  }
-  auto h_of = [&](const Cand4& k) -> uint32_t { return (k.word & kLeafBit) ? 0u : height[k.word]; };
-  struct Job {
-    uint32_t v2, slot4, pushes;  // BVH2 node, the BVH4 node to fill, pushes of the strict ancestors
-  };
-  const uint32_t root4 = (uint32_t)out->size();
-  out->emplace_back();
-  std::vector<Job> jobs{{root, root4, 0}};
-  while (!jobs.empty()) {
-    const Job jb = jobs.back();
-    jobs.pop_back();
-    std::vector<Cand4> cs;
-    for (int c = 0; c < 2; c++)
-      if (!empty_leaf(nodes[jb.v2].child[c])) cs.push_back(child_cand(nodes[jb.v2], c));
-    // every inner child's subtree, walked as the binary tree below it, must fit
-    auto fits = [&](const std::vector<Cand4>& set) {
-      if (full) return true;
-      const uint32_t p = jb.pushes + (uint32_t)set.size() - 1;
-      if (p > kTraversalStack) return false;
-      for (const Cand4& k : set)
-        if (p + h_of(k) > kTraversalStack) return false;
-      return true;
-    };
-    while (cs.size() < 4) {
-      int best = -1;
-      for (int i = 0; i < (int)cs.size(); i++)
-        if (!(cs[i].word & kLeafBit) && (best < 0 || cs[i].area > cs[best].area)) best = i;
-      if (best < 0) break;
-      std::vector<Cand4> trial;
-      for (int i = 0; i < (int)cs.size(); i++)
-        if (i != best) trial.push_back(cs[i]);
-      const BvhNode& e = nodes[cs[best].word];
-      for (int c = 0; c < 2; c++)
-        if (!empty_leaf(e.child[c])) trial.push_back(child_cand(e, c));
-      if (trial.size() > 4 || !fits(trial)) break;
-      cs = std::move(trial);
-    }
-    Bvh4Node nd;
-    for (int i = 0; i < 4; i++) {
-      nd.lo_x[i] = nd.lo_y[i] = nd.lo_z[i] = nd.hi_x[i] = nd.hi_y[i] = nd.hi_z[i] = 3e30f;
-      nd.child[i] = kLeafBit;  // an empty leaf: never hit (the box above), never tested
-      nd.pad[i] = 0;
-    }
-    const uint32_t pushes = jb.pushes + (cs.empty() ? 0u : (uint32_t)cs.size() - 1);
-    for (int i = 0; i < (int)cs.size(); i++) {
-      nd.lo_x[i] = cs[i].lo[0];
-      nd.lo_y[i] = cs[i].lo[1];
-      nd.lo_z[i] = cs[i].lo[2];
-      nd.hi_x[i] = cs[i].hi[0];
-      nd.hi_y[i] = cs[i].hi[1];
-      nd.hi_z[i] = cs[i].hi[2];
-      if (cs[i].word & kLeafBit) {
-        nd.child[i] = cs[i].word;
-      } else {
-        nd.child[i] = (uint32_t)out->size();
-        out->emplace_back();
-        jobs.push_back({cs[i].word, nd.child[i], pushes});
-      }
-    }
-    (*out)[jb.slot4] = nd;
-  }
-  // R per node (pad[0]): children before parents in reverse creation order
-  for (size_t i = out->size(); i-- > root4;) {
-    Bvh4Node& nd = (*out)[i];
-    uint32_t r = 0;
-    for (int c = 0; c < 4; c++)
-      if (!(nd.child[c] & kLeafBit)) r = std::max(r, 1 + (*out)[nd.child[c]].pad[0]);
-    nd.pad[0] = r;
-  }
-  return root4;
-}
-
 }  // namespace fs

@@ -67,33 +67,6 @@ FS_HD uint32_t leaf_word(uint32_t count, uint32_t first) {
   return kLeafBit | (count << kLeafCountShift) | first;
 }
 FS_HD uint32_t leaf_count(uint32_t w) { return (w >> kLeafCountShift) & 0xFu; }
-// BVH4 node, 128 B (one cache line): four child boxes, SoA over the children,
-// and four child words (the BVH2 child-word encoding). Built by collapsing
-// the BVH2 (collapse_bvh4); unused slots hold the never-hit box at 3e30 and
-// an empty leaf word.
-struct Bvh4Node {
-  float lo_x[4], hi_x[4];
-  float lo_y[4], hi_y[4];
-  float lo_z[4], hi_z[4];
-  uint32_t child[4];
-  uint32_t pad[4];
-};
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
-// BVH4 node with half-precision boxes, 80 B: the children's planes relative to
-// the node's origin (the low corner of their union), rounded outward to fp16
-// (one more fp16 step outward as a margin), packed two children per word:
-// px[0] = lo_x of children 0|1, px[1] = lo_x 2|3, px[2] = hi_x 0|1, px[3] = hi_x
-// 2|3; unused slots hold +inf planes (never hit). The walk reads them with
-// v_fma_mix_f32 (fp16 operands, fp32 arithmetic): one instruction per plane,
-// as the fp32 node, at 19 instead of 28 registers of node data.
-struct Bvh4HNode {
-  float org[3];
-  uint32_t pad;
-  uint32_t px[4], py[4], pz[4];
-  uint32_t child[4];
-};
-static_assert(sizeof(Bvh4HNode) == 80, "Bvh4HNode layout");
-Bvh4HNode compress_bvh4h(const Bvh4Node& n);
 constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces); the LDS stack bounds the waves per CU
 constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
@@ -179,21 +152,6 @@ struct BuildOptions {
   bool log = false;             // build phases to stderr
   static BuildOptions from(const fs_options* o);  // NULL: the defaults
 };
-
-// Collapses the BVH2 of one mesh (root `root` in nodes[0, n)) into BVH4 nodes
-// appended to *out; returns the BVH4 root index. Each BVH4 node takes the
-// children of a BVH2 node and repeatedly replaces its largest-area inner
-// child by that child's two children, up to four, as long as every walk's
-// stack need stays within kTraversalStack entries: a walk holds, at a node,
-// the un-popped siblings of its ancestors, so along every root-to-node path
-// the sum of (children - 1) must fit, counting the binary BVH2 height of the
-// subtrees below. The leaves (triangle slots) are the BVH2's.
-// full: no stack budget (every node takes up to four children); the walk
-// then bounds its stack at run time with revisit entries (fs_device.hip), and
-// each node's pad[0] holds R, the stack entries a walk below it may need
-// when every node pushes one entry (the BVH4 height below it).
-uint32_t collapse_bvh4(const BvhNode* nodes, size_t n, uint32_t root, std::vector<Bvh4Node>* out,
-                       bool full = false);
 
 // Restates the object constructors (object.cpp, mesh.cpp:168-275) and builds
 // one SAH BVH per mesh. Returns FS_OK or an fs_status with *err set.
