@@ -511,19 +511,17 @@ __device__ __forceinline__ T* at_byte(T* base, uint32_t off) {
 }
 
 // The material index of every bounce of a path, for the backward pass. Up to
-// 255 materials: 8-bit ids packed in two registers. More (MMAT): one u32 per
-// bounce in a per-lane scratch row ([level][lane] per wave), so scenes with
-// any number of materials render (scene.cpp:251-310 has no limit) and the
-// common case keeps its registers.
+// 255 materials: 8-bit ids packed in two registers, stored with the path's
+// end (PathRecords::mats). More (MMAT): the forward pass stores one u32 per
+// bounce in the record's id plane and keeps only level 0's here, so scenes
+// with any number of materials render (scene.cpp:251-310 has no limit) and
+// the common case keeps its registers.
 template <bool MMAT>
 struct MatTrail {
   uint32_t lo = 0, hi = 0;
-  uint32_t* row = nullptr;  // MMAT: the wave's row base
-  uint32_t lane = 0;
   __device__ __forceinline__ void reset() { lo = hi = 0; }
   __device__ __forceinline__ void set(uint32_t k, uint32_t mi) {
     if (MMAT) {
-      *at_byte(row, (k * kBlock + lane) * 4u) = mi;
       if (k == 0) lo = mi;
     } else if (k < 4) {
       lo |= mi << (8 * k);
@@ -531,10 +529,7 @@ struct MatTrail {
       hi |= mi << (8 * (k - 4));
     }
   }
-  __device__ __forceinline__ uint32_t get(int k) const {
-    if (MMAT) return k == 0 ? lo : *at_byte(row, ((uint32_t)k * kBlock + lane) * 4u);
-    return (k < 4 ? (lo >> (8 * k)) : (hi >> (8 * (k - 4)))) & 0xFFu;
-  }
+  __device__ __forceinline__ uint32_t get0() const { return MMAT ? lo : lo & 0xFFu; }
 };
 
 // engine.cpp:210-244: jittered ray through the pixel, optional thin lens.
@@ -564,144 +559,77 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
   return r;
 }
 
-// One sample = TracePixel (engine.cpp:161-164) after the ray generation of
-// engine.cpp:210-244. Returns the TraceResult colour.
-// Backward pass: Material::Sample in the order the TraceStep recursion
-// returns (engine.cpp:141-156); L enters as the radiance of level `top`+1.
-
-// texrow: per-level SampleDiffuse result of a textured material (lean kernel
-// only; other schedules pass nullptr and never see a textured scene).
-// The loads of level k-1 (its material's kind and colour, its c) are issued
-// before level k is applied, so the serial chain of the backward pass waits
-// on one cache round trip per path instead of one per level.
-// SELECTS: Material::Sample as straight-line selects (the kernels without
-// parked walks: C2 +2.3 %, C3 +0.9 %) or as a per-kind switch (the parked-walk
-// kernel: the selects cost C4 0.9 %).
-// LROWS: the rows are lane-major ([lane][level], HBM rows of the walk
-// kernels): the path's eight c values arrive in two 16-B loads before the
-// first level, and the level loop runs unrolled over wave-uniform levels
-// (constant register indices), so only the hot material records stay on each
-// level's critical path, not an L2 round trip to the row.
-template <bool LROWS>
-__device__ __forceinline__ uint32_t row_off(uint32_t level, uint32_t lane, bool hi, uint32_t stride = kBlock) {
-  if (LROWS) return (hi ? kMaxDepth * kBlock : 0u) + lane * kMaxDepth + level;
-  return ((hi ? kMaxDepth : 0u) + level) * stride + lane;
+// The path record of sample `slot` (its low bits: s * 64 + 8 * py + px) of
+// the block whose record row is `row`.
+__device__ __forceinline__ uint64_t rec_index(const Launch& P, uint32_t row, uint32_t slot) {
+  return (uint64_t)row * (P.spp * kBlock) + (slot & 0x3FFFFFFFu);
 }
-template <bool TEX = false, bool MMAT = false, bool SELECTS = false, bool LROWS = false>
-__device__ __forceinline__ f3 unwind(const DevScene& S, f3 L, int top, const MatTrail<MMAT>& mats,
-                                     const float2* __restrict__ lvl, f3 p0, f3 lp0, uint64_t& rng,
-                                     int stride = kBlock, uint32_t lane = 0,
-                                     const float4* __restrict__ texrow = nullptr) {
-  if (top < 0) return L;
-  const float* cv = reinterpret_cast<const float*>(lvl);
-  // c = max(0, n.r) of every kind: [level][lane]; Ceramic's specular term: [kMaxDepth + level][lane]
-  const fs_material* mp = &S.materials[mats.get(top)];
-  int32_t kind = mp->kind;
-  f3 dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
-  float cs[kMaxDepth];
-  float c = 0.0f;
-  // (Metal's roughness and Ceramic's specular term loaded one level ahead
-  // with the material: C3 -2.4 %, C4 -1.6 %, profiles/r03/ab_unwind_pipe.log)
-  if constexpr (LROWS) {
-    static_assert(kMaxDepth == 8, "two 16-B loads per lane");
-    const float4* q = reinterpret_cast<const float4*>(at_byte(cv, lane * (kMaxDepth * 4u)));
-    const float4 a = q[0], b = q[1];
-    cs[0] = a.x, cs[1] = a.y, cs[2] = a.z, cs[3] = a.w, cs[4] = b.x, cs[5] = b.y, cs[6] = b.z, cs[7] = b.w;
-    // (the specular terms of a Ceramic/Glow path as two more loads: C3 -7.6 %,
-    // C4 -2.4 %, spills 60 -> 76 B/lane; they stay loads at their level)
-  } else {
-    c = *at_byte(cv, ((uint32_t)top * (uint32_t)stride + lane) * 4u);
-  }
+
+// FogMaterial::Sample's draw at level 0 (material.cpp:319-339): true when
+// the diffuse colour replaces the incoming light. p0, lp0: the path's first
+// two hit points (the second is the segment's end on a miss).
+__device__ __forceinline__ bool fog_takes_diffuse(const fs_material& m, f3 p0, f3 lp0, uint64_t& rng) {
+  float dist = length(p0 - lp0);
+  float x = (dist * dist) * m.density * 0.00005f;
+  float mx = (0.0f < x) ? x : 0.0f;
+  float th = (mx < 0.0f) ? 0.0f : (mx > 1.0f ? 1.0f : mx);
+  return rng_float(rng) < th;
+}
+
+// The backward pass of one path (engine.cpp:141-156): Material::Sample of
+// levels top .. 0 in the order the TraceStep recursion returns. L enters as
+// the radiance of level top + 1; c holds the path's c values (levels
+// <= top), M the backward-pass material table (DevScene::umat, in LDS or
+// global memory). Levels run unrolled over wave-uniform indices (each lane
+// applies the levels <= its top), and every kind is one straight-line
+// sequence of selects, each kind's operations in the reference's order:
+//   Diffuse  (sd*L)*c                     Metal  ((sd*L)*c)*r + (sd*L)*(1-r)
+//   Mirror/Glass/Liquid  L*dif            Ceramic  L*ds + ((sd*L)*c)*(1-ds) (+glow)
+//   Light  emissive (its texel when mapped), Fog  L or, at level 0, dif when
+//   the forward pass's draw said so (kRecFogDif)
+template <bool TEX, bool MMAT, class MatPtr>
+__device__ __forceinline__ f3 unwind_path(MatPtr M, const PathRecords& R, uint64_t q, f3 L, int top, bool fog_dif,
+                                          uint2 packed, const float (&c)[kMaxDepth]) {
+  int32_t kind0 = 0;
 #pragma unroll
-  for (int lv = (LROWS ? (int)kMaxDepth - 1 : 0); lv >= 0; --lv) {
-   const int k0 = LROWS ? lv : top;
-   if (LROWS && lv > top) continue;
-   for (int k = k0; k >= (LROWS ? lv : 0); --k) {
-    const fs_material& m = *mp;
-    const int32_t kk = kind;
-    const f3 dk = dif;
-    const float ck = LROWS ? cs[LROWS ? lv : 0] : c;
-    if (k > 0) {  // next level's loads, in flight while this level is applied
-      mp = &S.materials[mats.get(k - 1)];
-      kind = mp->kind;
-      dif = mk3(mp->diffuse[0], mp->diffuse[1], mp->diffuse[2]);
-      if (!LROWS) c = *at_byte(cv, ((uint32_t)(k - 1) * (uint32_t)stride + lane) * 4u);
-    }
+  for (int k = (int)kMaxDepth - 1; k >= 0; --k) {
+    if (k > top) continue;
+    const uint32_t id = MMAT ? R.mat[(uint64_t)k * R.n + q]
+                             : ((k < 4 ? (packed.x >> (8 * k)) : (packed.y >> (8 * (k - 4)))) & 0xFFu);
+    const float4 m0 = M[3 * id], m1 = M[3 * id + 1];
+    const int32_t kk = __float_as_int(m0.x);
+    const f3 dk = mk3(m0.y, m0.z, m0.w);
     f3 sd = dk;  // SampleDiffuse (material.cpp:108-126)
-    if (TEX && m.texture >= 0) {
-      float4 tx = *at_byte(texrow, ((uint32_t)k * (uint32_t)stride + lane) * 16u);
-      sd = mk3(tx.x, tx.y, tx.z);
-    }
-    if constexpr (SELECTS) {
-      // Material::Sample of every kind as one straight-line sequence (selects,
-      // not a per-kind branch), each kind's operations in the reference's order:
-      //   Diffuse  (sd*L)*c                     Metal  ((sd*L)*c)*r + (sd*L)*(1-r)
-      //   Mirror/Glass/Liquid  L*dif            Ceramic  L*ds + ((sd*L)*c)*(1-ds) (+glow)
-      //   Light  emissive (its texel when mapped), Fog  L or, at level 0, dif by a draw
-      const bool mirrorish = kk == FS_MAT_MIRROR || kk == FS_MAT_GLASS || kk == FS_MAT_LIQUID;
-      const bool metal = kk == FS_MAT_METAL, cer = kk == FS_MAT_CERAMIC || kk == FS_MAT_GLOW;
-      float wa = 0.0f, wb = 0.0f;  // the two weights of Metal and Ceramic
-      if (metal || cer) {
-        wa = metal ? m.roughness : *at_byte(cv, row_off<LROWS>((uint32_t)k, lane, true, (uint32_t)stride) * 4u);
-        wb = (float)(1.0 - (double)wa);
-      }
-      const f3 t = (mirrorish ? dk : sd) * L;  // L*dif is dif*L bit for bit
-      const f3 dc = t * ck;
-      f3 mix = (metal ? dc : L) * wa + (metal ? t : dc) * wb;
-      if (kk == FS_MAT_GLOW) mix = mix + mk3(m.glow[0], m.glow[1], m.glow[2]);
-      f3 out = kk == FS_MAT_DIFFUSE ? dc : ((metal || cer) ? mix : (mirrorish ? t : L));
-      if (kk == FS_MAT_LIGHT)  // material.cpp:43-53
-        out = (TEX && m.texture >= 0) ? sd : mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
-      if (kk == FS_MAT_FOG && k == 0) {  // material.cpp:319-339
-        float dist = length(p0 - lp0);
-        float x = (dist * dist) * m.density * 0.00005f;
-        float mx = (0.0f < x) ? x : 0.0f;
-        float th = (mx < 0.0f) ? 0.0f : (mx > 1.0f ? 1.0f : mx);
-        if (rng_float(rng) < th) out = dk;
-      }
-      L = out;
-    } else {
-      switch (kk) {
-        case FS_MAT_LIGHT:  // material.cpp:43-53
-          L = (TEX && m.texture >= 0) ? sd : mk3(m.emissive[0], m.emissive[1], m.emissive[2]);
-          break;
-        case FS_MAT_DIFFUSE:
-          L = (sd * L) * ck;
-          break;
-        case FS_MAT_METAL: {
-          f3 dc = (sd * L) * ck;
-          f3 rc = sd * L;
-          L = dc * m.roughness + rc * (float)(1.0 - (double)m.roughness);
-          break;
-        }
-        case FS_MAT_MIRROR:
-        case FS_MAT_GLASS:
-        case FS_MAT_LIQUID:
-          L = L * dk;
-          break;
-        case FS_MAT_CERAMIC:
-        case FS_MAT_GLOW: {
-          const float ds = *at_byte(cv, row_off<LROWS>((uint32_t)k, lane, true, (uint32_t)stride) * 4u);
-          f3 dc = (sd * L) * ck;
-          L = L * ds + dc * (float)(1.0 - (double)ds);
-          if (kk == FS_MAT_GLOW) L = L + mk3(m.glow[0], m.glow[1], m.glow[2]);
-          break;
-        }
-        default:  // FS_MAT_FOG (material.cpp:319-339)
-          if (k == 0) {
-            float dist = length(p0 - lp0);
-            float x = (dist * dist) * m.density * 0.00005f;
-            float mx = (0.0f < x) ? x : 0.0f;
-            float th = (mx < 0.0f) ? 0.0f : (mx > 1.0f ? 1.0f : mx);
-            if (rng_float(rng) < th) L = dk;
-          }
-          break;
+    bool mapped = false;
+    if (TEX) {
+      mapped = __float_as_int(M[3 * id + 2].w) >= 0;
+      if (mapped) {
+        const float4 tx = R.tex[(uint64_t)k * R.n + q];
+        sd = mk3(tx.x, tx.y, tx.z);
       }
     }
-   }
+    const bool mirrorish = kk == FS_MAT_MIRROR || kk == FS_MAT_GLASS || kk == FS_MAT_LIQUID;
+    const bool metal = kk == FS_MAT_METAL, cer = kk == FS_MAT_CERAMIC || kk == FS_MAT_GLOW;
+    float wa = 0.0f;  // the two weights of Metal and Ceramic
+    if (metal) wa = m1.x;
+    if (cer) wa = R.ds[(uint64_t)k * R.n + q];
+    const float wb = (float)(1.0 - (double)wa);
+    const f3 t = (mirrorish ? dk : sd) * L;  // L*dif is dif*L bit for bit
+    const f3 dc = t * c[k];
+    f3 mix = (metal ? dc : L) * wa + (metal ? t : dc) * wb;
+    if (kk == FS_MAT_GLOW) {
+      const float4 m2 = M[3 * id + 2];
+      mix = mix + mk3(m2.x, m2.y, m2.z);
+    }
+    f3 out = kk == FS_MAT_DIFFUSE ? dc : ((metal || cer) ? mix : (mirrorish ? t : L));
+    if (kk == FS_MAT_LIGHT)  // material.cpp:43-53
+      out = (TEX && mapped) ? sd : mk3(m1.y, m1.z, m1.w);
+    if (kk == FS_MAT_FOG && k == 0 && fog_dif) out = dk;
+    L = out;
+    if (k == 0) kind0 = kk;
   }
-  // engine.cpp:147-151 (kind holds level 0's: the loop ends on it)
-  if (length(L) > 10.0f && kind == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
+  // engine.cpp:147-151 (level 0's kind)
+  if (top >= 0 && length(L) > 10.0f && kind0 == FS_MAT_LIGHT) L = normalize(L) * (float)10.0;
   return L;
 }
 
@@ -1223,8 +1151,12 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         if (visit)
           small_mesh_trace<COUNT>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
 #ifdef FS_PHASE_PROF
-        pa.small += FS_TICK() - t1;
-        t1 = FS_TICK();
+        {  // the faces are their own phase: neither the cull's nor the walk's
+          const uint64_t ts = FS_TICK() - t1;
+          pa.small += ts;
+          t0 += ts;
+          t1 += ts;
+        }
 #endif
       } else if (NOWALK) {
         // every mesh of the scene is small (chosen at upload): no BVH walk
@@ -1544,14 +1476,6 @@ __device__ __forceinline__ const T& at_use(const T& v, uint32_t zero) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(&v) + zero);
 }
 
-// One sample's radiance, 12 contiguous bytes of its block's radiance row
-// (streaming stores measured the same: C2/C3/C4 within 0.2 %).
-__device__ __forceinline__ void store_rgb(float* p, f3 L) {
-  p[0] = L.x;
-  p[1] = L.y;
-  p[2] = L.z;
-}
-
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kFog0 = 0x40000000u;  // slot bit: the first hit is Fog
 constexpr uint32_t kQueueStride = 64;  // work-queue counters 256 B apart
@@ -1580,10 +1504,13 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
   return kNoBlock;
 }
 
-// The path-trace megakernel: path regeneration with a lean register
-// footprint. The closest-hit query keeps only (t, object, primitive, u, v);
-// the per-bounce shading scalars and the Fog anchors live in per-lane
-// scratch rows of the wave; the depth-0 AOVs go straight to the frame.
+// The path-trace megakernel: the forward pass of every path, with path
+// regeneration and a lean register footprint. The closest-hit query keeps
+// only (t, object, primitive, u, v); each bounce's shading scalars go to the
+// sample's path record and a finished path leaves its end state there
+// (PathRecords); fold_paths runs the backward passes afterwards on full
+// waves. The Fog anchors live in per-lane scratch rows of the wave; the
+// depth-0 AOVs go straight to the frame.
 //
 // Work: the wave's lanes share one pool of (pixel, sample) tasks. Whenever
 // lanes are free (their path ended) they take the next tasks of the wave's
@@ -1592,46 +1519,33 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 // handing out its tasks, so lanes never wait for a block's stragglers. With
 // P.persist the grid is one wave per wave slot of the chip and the waves
 // pull blocks until every queue is empty: the launch tail is one task
-// path, not one block. Each sample's radiance goes to its block's radiance
-// row; fold_groups folds the rows into the frame in sample order.
+// path, not one block. fold_paths folds the records into the frame in
+// sample order.
 //
-// NOWALK (every mesh small): no walk stack; the per-bounce shading scalars
-// (c and Ceramic's term, [level][lane]) are staged in LDS instead of HBM
-// scratch rows, so the backward pass reads them at LDS latency and the L2
-// no longer holds (and writes back) the rows. SUSP (the parked-walk kernel):
-// the HBM rows are lane-major ([lane][level]), so the backward pass loads a
-// path's eight c values in two 16-B loads (C4 +3.5 %).
+// NOWALK (every mesh small): no walk stack and 8 waves per SIMD.
 template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false,
           bool NOWALK = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
-                                                                    float2* __restrict__ lvl_all,
+                                                                    PathRecords R,
                                                                     float4* __restrict__ anchor_all,
-                                                                    float4* __restrict__ tex_all,
-                                                                    float* __restrict__ rad_all,
-                                                                    uint32_t* __restrict__ mat_all,
                                                                     uint32_t* __restrict__ queues,
                                                                     DevCounters* __restrict__ counters) {
-  constexpr bool kLdsRows = NOWALK;
-  constexpr bool kLaneRows = !kLdsRows && SUSP;  // HBM rows lane-major (unwind's LROWS)
   __shared__ uint32_t stk_all[NOWALK ? 1 : kTraversalStack * kBlock];
-  __shared__ float2 lvl_lds[kLdsRows ? kMaxDepth * kBlock : 1];
   const uint32_t lane = threadIdx.x % kBlock;
   const uint32_t wid = blockIdx.x;  // this wave's rows
   Tally<COUNT> tally;
   uint32_t* stk = stk_all + lane;
-  // Scratch rows of the wave, addressed as wave base (SGPR) + 32-bit lane offset.
-  float2* lvl = kLdsRows ? lvl_lds : lvl_all + (size_t)wid * (kMaxDepth * kBlock);
+  // The Fog anchor rows of the wave, addressed as wave base (SGPR) + 32-bit lane offset.
   float4* anchor = anchor_all + (size_t)wid * (2 * kBlock);  // [0]: p0.xyz, [1]: lp0.xyz
   const uint32_t a0_off = lane * 16u, a1_off = (kBlock + lane) * 16u;
-  float4* texrow = tex_all + (size_t)wid * (kMaxDepth * kBlock);  // only touched by textured scenes
 
   TaskBlock cur;  // the block the wave hands out tasks from
   uint32_t queue = blockIdx.x & 7u, queues_left = P.persist ? 8u : 1u;
   uint32_t segments = 0, samples_done = 0;
 
-  // the lane's task: its pixel, sample and radiance slot
+  // the lane's task: its pixel, sample and record slot
   uint32_t x = 0, y = 0, pix = 0, smp = 0;
-  uint32_t rad_row = 0;
+  uint32_t rad_row = 0;  // the block's record row: the path record is q = rad_row * spp * 64 + slot's low bits
   // s * kBlock + 8 * py + px; bit 31: this sample leaves the AOVs; bit 30
   // (kFog0): the path's first hit is Fog, so its two anchors are kept
   uint32_t slot = 0;
@@ -1639,8 +1553,6 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   Ray r;
   uint32_t depth = 0;
   MatTrail<MMAT> mats;
-  mats.row = MMAT ? mat_all + (size_t)wid * (kMaxDepth * kBlock) : nullptr;
-  mats.lane = lane;
   int top = -1;
   bool fresh = true;
   MinHit h;         // persists across iterations while a walk is parked (SUSP)
@@ -1768,9 +1680,10 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         rebuild_hit<TEX>(S, r, h, p, nn, mi, tu, tv, stk);
         if (depth == 1 && (slot & kFog0)) *at_byte(anchor, a1_off) = make_float4(p.x, p.y, p.z, 0);
         const fs_material& m = S.materials[mi];
+        const uint64_t q = rec_index(P, rad_row, slot);
         if (TEX && m.texture >= 0) {
           f3 tx = sample_tex(S, m, tu, tv);
-          *at_byte(texrow, (depth * kBlock + lane) * 16u) = make_float4(tx.x, tx.y, tx.z, 0.0f);
+          R.tex[depth * R.n + q] = make_float4(tx.x, tx.y, tx.z, 0.0f);
         }
         int32_t kind = m.kind;
         f3 view = normalize(p - r.start);
@@ -1781,9 +1694,9 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
-        *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, false) * 4u) = c;
-        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW)
-          *at_byte(reinterpret_cast<float*>(lvl), row_off<kLaneRows>(depth, lane, true) * 4u) = ds;
+        R.c[depth * R.n + q] = c;
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) R.ds[depth * R.n + q] = ds;
+        if (MMAT) R.mat[depth * R.n + q] = (uint32_t)mi;
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
         if (depth == 0 && kind == FS_MAT_FOG) {  // Fog draws with the distance of its two anchors
@@ -1819,18 +1732,20 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     if (done) act[3] += (uint64_t)(top + 1);
 #endif
     if (done) {
-      f3 p0 = mk3(0, 0, 0), lp0 = mk3(0, 0, 0);
-      if (slot & kFog0) {  // both anchors were written (a Fog hit always bounces on to depth 1)
-        float4 a = *at_byte(anchor, a0_off), b = *at_byte(anchor, a1_off);
-        p0 = mk3(a.x, a.y, a.z);
-        lp0 = mk3(b.x, b.y, b.z);
+      // The path's end state: the radiance entering level top + 1, top, and
+      // the packed material ids; fold_paths applies the levels.
+      uint32_t meta = (uint32_t)(top + 1);
+      if (slot & kFog0) {
+        // Fog at level 0 (material.cpp:319-339) draws after every level above
+        // it has been applied, i.e. after the forward pass's last draw: the
+        // draw is taken here and the record keeps its outcome.
+        const float4 a = *at_byte(anchor, a0_off), b = *at_byte(anchor, a1_off);
+        const fs_material& m0 = S.materials[mats.get0()];
+        if (fog_takes_diffuse(m0, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), rng)) meta |= kRecFogDif;
       }
-      L = unwind<TEX, MMAT, !SUSP, kLaneRows>(S, L, top, mats, lvl, p0, lp0, rng, kBlock, lane, texrow);
-      // [sample][pixel][channel]: one 12-B record per sample (the planar
-      // [channel][sample][pixel] rows wrote 50 B per sample back from L2)
-      float* rad = rad_all + (size_t)rad_row * (3 * P.spp * kBlock);
-      const uint32_t o = slot & ~(0x80000000u | kFog0);
-      store_rgb(rad + 3 * o, L);
+      const uint64_t q = rec_index(P, rad_row, slot);
+      R.end[q] = make_float4(L.x, L.y, L.z, __uint_as_float(meta));
+      if (!MMAT && top >= 0) R.mats[q] = make_uint2(mats.lo, mats.hi);
       if (COUNT) samples_done++;
       fresh = true;
     }
@@ -1865,14 +1780,28 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   }
 }
 
-// Folds the radiance rows of a launch into the frame: block b is micro-tile
-// b of group 0 (decode_block's tile-major order without the XCD placement
-// or tile order), lane = pixel; group g's rows are row g * gridDim.x + b.
-// Each pixel folds its samples in sample order (frame.cpp:53-63), so the
+// The backward passes of a launch and their fold into the frame: block b is
+// micro-tile b of group 0 (decode_block's tile-major order without the XCD
+// placement or tile order), lane = pixel; group g's records are row
+// g * gridDim.x + b. Each pixel runs its samples' backward passes
+// (unwind_path) and folds them in sample order (frame.cpp:53-63), so the
 // frame is bit-identical to groups x spp consecutive TraceScene calls.
-// HBM-bound: 12 B read per sample plus one frame row.
-__global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, const float* __restrict__ rad_all) {
+// The loads are pipelined across samples: while sample i is unwound, the c
+// values of sample i + 1 (whose end record arrived one sample earlier) and
+// the end record and material ids of sample i + 2 are in flight, and the
+// material table sits in LDS (LDSM), so a sample waits on no memory round
+// trip of its own.
+// (LDSM: 48 B of dynamic LDS per material; up to 64 materials, so that LDS
+// does not limit the waves per CU).
+constexpr uint32_t kFoldLdsMaterials = 64;
+template <bool TEX, bool MMAT, bool LDSM>
+__global__ __launch_bounds__(kBlock) void fold_paths(DevScene S, DevFrame F, Launch P, PathRecords R) {
+  extern __shared__ float4 mat_lds[];
   const uint32_t lane = threadIdx.x, b = blockIdx.x;
+  if (LDSM) {
+    for (uint32_t i = lane; i < 3 * S.num_materials; i += kBlock) mat_lds[i] = S.umat[i];
+    __syncthreads();
+  }
   const uint32_t micro_per_side = P.tile_size / 8, micro_per_tile = micro_per_side * micro_per_side;
   const uint32_t owned = b / micro_per_tile, micro = b % micro_per_tile;
   const uint32_t tile = P.tile_offset + owned * P.tile_stride;
@@ -1882,15 +1811,51 @@ __global__ __launch_bounds__(kBlock) void fold_groups(DevFrame F, Launch P, cons
   const size_t pix = (size_t)y * F.width + x;
   f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
   uint32_t n = F.count[pix];
-  for (uint32_t g = 0; g < P.groups; g++) {
-    const float* rad = rad_all + ((size_t)g * gridDim.x + b) * (3 * P.spp * kBlock);
-    for (uint32_t k = 0; k < P.spp; k++) {
-      const uint32_t o = k * kBlock + lane;
-      f3 L = mk3(rad[3 * o], rad[3 * o + 1], rad[3 * o + 2]);
-      f3 np = mean * (float)n + L;
-      float dv = (float)(++n);
-      mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+  const uint32_t total = P.groups * P.spp;
+  auto rec = [&](uint32_t i) {  // sample i of the pixel: group i / spp, sample i % spp
+    const uint32_t g = i / P.spp, k = i - g * P.spp;
+    return rec_index(P, g * gridDim.x + b, k * kBlock + lane);
+  };
+  auto load_c = [&](uint64_t q, int top, float (&c)[kMaxDepth]) {
+#pragma unroll
+    for (int k = 0; k < (int)kMaxDepth; k++) c[k] = k <= top ? R.c[(uint64_t)k * R.n + q] : 0.0f;
+  };
+  auto top_of = [](const float4& e) { return (int)(__float_as_uint(e.w) & 0xFFu) - 1; };
+  const uint2 none = make_uint2(0u, 0u);
+  // sample i (a), i + 1 (b), i + 2 (e2, m2)
+  uint64_t qa = rec(0), qb = total > 1 ? rec(1) : qa;
+  float4 ea = R.end[qa], eb = R.end[qb];
+  uint2 ma = MMAT ? none : R.mats[qa], mb = MMAT ? none : R.mats[qb];
+  float ca[kMaxDepth], cb[kMaxDepth];
+  load_c(qa, top_of(ea), ca);
+  for (uint32_t i = 0; i < total; i++) {
+    uint64_t q2 = qb;
+    float4 e2 = eb;
+    uint2 m2 = mb;
+    if (i + 1 < total) load_c(qb, top_of(eb), cb);
+    if (i + 2 < total) {
+      q2 = rec(i + 2);
+      e2 = R.end[q2];
+      if (!MMAT) m2 = R.mats[q2];
     }
+    const uint32_t meta = __float_as_uint(ea.w);
+    f3 L;
+    if (LDSM)
+      L = unwind_path<TEX, MMAT>(static_cast<const float4*>(mat_lds), R, qa, mk3(ea.x, ea.y, ea.z), top_of(ea),
+                                 (meta & kRecFogDif) != 0, ma, ca);
+    else
+      L = unwind_path<TEX, MMAT>(S.umat, R, qa, mk3(ea.x, ea.y, ea.z), top_of(ea), (meta & kRecFogDif) != 0, ma, ca);
+    f3 np = mean * (float)n + L;
+    float dv = (float)(++n);
+    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+    qa = qb;
+    ea = eb;
+    ma = mb;
+#pragma unroll
+    for (int k = 0; k < (int)kMaxDepth; k++) ca[k] = cb[k];
+    qb = q2;
+    eb = e2;
+    mb = m2;
   }
   F.color[3 * pix] = mean.x;
   F.color[3 * pix + 1] = mean.y;
@@ -2036,7 +2001,7 @@ struct fs_context {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool have_scene = false;
-  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, table, counters, pack_send, tile_order,
+  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, umat, table, counters, pack_send, tile_order,
       pack_recv, range_io, tree, tree_objs;
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
@@ -2057,7 +2022,7 @@ struct fs_context {
   float last_ms = 0.0f;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  DevBuf rows;  // per-lane scratch rows of the lean kernel (LeanRows)
+  DevBuf rows;  // the Fog anchor rows and the path records of a render (path_records)
   DevBuf queues;  // per-XCD work-queue counters of the persistent trace kernel
   uint32_t cus = 0;  // compute units: the persistent grid is one wave per wave slot
 };
@@ -2134,27 +2099,22 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
   return b;
 }
 
-// Scratch of the lean kernel, carved out of one allocation: per wave of the
-// grid, the per-lane rows of the shading scalars (lvl), the Fog anchors, the
-// texels (textured scenes) and the material ids (MMAT); per block of the
-// launch, the radiance rows of its samples (read by fold_groups).
-struct LeanRows {
-  float2* lvl = nullptr;
-  float4* anchor = nullptr;
-  float4* tex = nullptr;
-  float* rad = nullptr;
-  uint32_t* mat = nullptr;
-};
-int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, uint32_t spp, LeanRows* W, bool tex_rows,
-              bool mat_rows) {
-  const size_t per = 8 * kMaxDepth + 32 + (tex_rows ? 16 * kMaxDepth : 0) + (mat_rows ? 4 * kMaxDepth : 0);
-  const size_t bytes = (size_t)wave_lanes * per + (size_t)block_lanes * 12 * spp + 5 * 256;  // + alignment
+// Scratch of a render, carved out of one allocation: per wave of the grid,
+// the per-lane Fog anchor rows; per sample of the launch, its path record
+// (PathRecords: c and Ceramic's term per level, the end state, the material
+// ids, and on textured scenes the texel per level).
+size_t record_bytes(bool tex, bool mmat) {
+  return 8 * kMaxDepth + 16 + (mmat ? 4 * kMaxDepth : 8) + (tex ? 16 * kMaxDepth : 0);
+}
+int path_records(fs_context* ctx, uint64_t wave_lanes, uint64_t samples, PathRecords* R, float4** anchors, bool tex,
+                 bool mmat) {
+  const size_t bytes = (size_t)wave_lanes * 32 + (size_t)samples * record_bytes(tex, mmat) + 6 * 256;  // + alignment
   // Shrink a buffer more than 4x (and 1 GiB) larger than this render needs:
-  // a context that once rendered a long launch does not keep its rows.
+  // a context that once rendered a long launch does not keep its records.
   if (ctx->rows.bytes > 4 * bytes && ctx->rows.bytes - bytes > (1ull << 30)) ctx->rows.release();
   if (ctx->rows.bytes < bytes) {
     int rc = ensure(&ctx->rows, bytes);
-    if (rc) return rc == FS_ERR_DEVICE ? fail(FS_ERR_NOMEM, "scratch rows: " + g_error) : rc;
+    if (rc) return rc == FS_ERR_DEVICE ? fail(FS_ERR_NOMEM, "path records: " + g_error) : rc;
   }
   char* p = (char*)ctx->rows.p;
   auto take = [&](size_t n) {
@@ -2162,13 +2122,16 @@ int lean_rows(fs_context* ctx, uint64_t wave_lanes, uint64_t block_lanes, uint32
     p += (n + 255) & ~(size_t)255;
     return q;
   };
-  *W = LeanRows{};
-  W->anchor = (float4*)take(32ull * wave_lanes);
-  W->lvl = (float2*)take(8ull * kMaxDepth * wave_lanes);
-  W->tex = tex_rows ? (float4*)take(16ull * kMaxDepth * wave_lanes) : nullptr;
-  W->rad = (float*)take(12ull * spp * block_lanes);
-  W->mat = mat_rows ? (uint32_t*)take(4ull * kMaxDepth * wave_lanes) : nullptr;
-  if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "scratch row overflow");
+  *R = PathRecords{};
+  *anchors = (float4*)take(32ull * wave_lanes);
+  R->n = samples;
+  R->c = (float*)take(4ull * kMaxDepth * samples);
+  R->ds = (float*)take(4ull * kMaxDepth * samples);
+  R->end = (float4*)take(16ull * samples);
+  R->mats = mmat ? nullptr : (uint2*)take(8ull * samples);
+  R->mat = mmat ? (uint32_t*)take(4ull * kMaxDepth * samples) : nullptr;
+  R->tex = tex ? (float4*)take(16ull * kMaxDepth * samples) : nullptr;
+  if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "path record overflow");
   return FS_OK;
 }
 
@@ -2234,8 +2197,7 @@ constexpr int kLeanWaves = 6, kSuspWaves = 6, kNowalkWaves = 8;
 // walks), MMAT (material ids in scratch rows), SOCT (object octree), NOWALK>.
 // Textured scenes never park. Names as rocprofv3 prints the uncounted ones
 // (fs_last_kernel).
-typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, float2*, float4*, float4*, float*, uint32_t*,
-                       uint32_t*, DevCounters*);
+typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, PathRecords, float4*, uint32_t*, DevCounters*);
 struct LeanKernel {
   LeanFn fn;
   const char* name;
@@ -2327,7 +2289,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
-                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->table, &ctx->range_io,
+                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->umat, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
   ctx->rows.release();
@@ -2411,6 +2373,21 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   if ((rc = upload(ctx, &ctx->tex_rgb, P.tex_rgb.data(), P.tex_rgb.size() * sizeof(float)))) return rc;
   if ((rc = upload(ctx, &ctx->tex_info, P.tex_info.data(), P.tex_info.size() * sizeof(uint32_t)))) return rc;
   if ((rc = upload(ctx, &ctx->materials, P.materials.data(), P.materials.size() * sizeof(fs_material)))) return rc;
+  {  // the backward pass's fields of every material (DevScene::umat)
+    auto __int_as_float = [](int32_t v) {
+      float f;
+      std::memcpy(&f, &v, 4);
+      return f;
+    };
+    std::vector<float4> um(3 * P.materials.size());
+    for (size_t i = 0; i < P.materials.size(); i++) {
+      const fs_material& m = P.materials[i];
+      um[3 * i] = make_float4(__int_as_float(m.kind), m.diffuse[0], m.diffuse[1], m.diffuse[2]);
+      um[3 * i + 1] = make_float4(m.roughness, m.emissive[0], m.emissive[1], m.emissive[2]);
+      um[3 * i + 2] = make_float4(m.glow[0], m.glow[1], m.glow[2], __int_as_float(m.texture));
+    }
+    if ((rc = upload(ctx, &ctx->umat, um.data(), um.size() * sizeof(float4)))) return rc;
+  }
   if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
   if ((rc = upload(ctx, &ctx->tree, &P.tree, P.tree_valid ? sizeof(DevSceneTree) : 0))) return rc;
   if ((rc = upload(ctx, &ctx->tree_objs, P.tree_objs.data(), P.tree_objs.size() * sizeof(uint32_t)))) return rc;
@@ -2449,6 +2426,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   S.tris = (const DevTri*)ctx->tris.p;
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
+  S.umat = (const float4*)ctx->umat.p;
+  S.num_materials = (uint32_t)P.materials.size();
   S.table = (const float4*)ctx->table.p;
   S.tri_tex = (const float2*)ctx->tri_tex.p;
   S.tex_rgb = (const float*)ctx->tex_rgb.p;
@@ -2614,18 +2593,22 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
   // Sample groups: a launch renders G runs of `chunk` samples as
-  // G x blocks blocks, then fold_groups folds them in order. Persistent
-  // waves have a launch tail of one task path, so G is as large as the
-  // radiance rows allow (kRadianceRowBytes: C4 at 1080p x 1024 spp is one
-  // launch, 25.7 GB of rows). One-shot waves size G so a launch holds
+  // G x blocks blocks, then fold_paths runs their backward passes and folds
+  // them in order. Persistent waves have a launch tail of one task path, so G
+  // is as large as the path records allow (kRecordBytes: C4 at 1080p x 1024
+  // spp is two launches of 512 spp). One-shot waves size G so a launch holds
   // >= kGroupTargetBlocks blocks (about 43 per wave slot of the chip).
   const uint32_t full_chunks = params->spp / chunk;
   uint32_t G = 1;
-  // The radiance rows of a persistent launch: at most kRadianceRowBytes and at
-  // most half of the device memory that is free (counting the rows this
+  const bool tree = ctx->scene.tree != nullptr;
+  const bool mm = ctx->many_materials || tree;
+  const bool tex_rec = ctx->has_textures || tree;
+  const size_t rec_bytes = record_bytes(tex_rec, mm);
+  // The path records of a persistent launch: at most kRecordBytes and at
+  // most half of the device memory that is free (counting the records this
   // context already holds), so a smaller or shared GPU renders in more,
   // smaller launches instead of failing.
-  uint64_t row_budget = kRadianceRowBytes;
+  uint64_t row_budget = kRecordBytes;
   {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
@@ -2633,7 +2616,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   }
   if (blocks && full_chunks > 1) {
     uint64_t want = O.groups  ? (uint64_t)O.groups
-                    : O.persist ? std::max<uint64_t>(1, row_budget / (blocks * 12ull * chunk * kBlock))
+                    : O.persist ? std::max<uint64_t>(1, row_budget / (blocks * rec_bytes * chunk * kBlock))
                                 : (kGroupTargetBlocks + blocks - 1) / blocks;
     want = std::max<uint64_t>(1, std::min<uint64_t>({want, full_chunks, ((1ull << 31) - 1) / blocks}));
     const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
@@ -2671,9 +2654,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   }
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
-  LeanRows rows;
-  const bool tree = ctx->scene.tree != nullptr;
-  const bool mm = ctx->many_materials || tree;
+  PathRecords rec;
+  float4* anchors = nullptr;
   const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr,
                                    ctx->has_walks || !O.lds_rows);
   // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
@@ -2681,9 +2663,9 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
   auto grid_for = [&](uint64_t nb) { return O.persist ? std::min<uint64_t>(wave_slots, nb) : nb; };
   if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
-  // On an allocation failure the launches shrink (G halved) until the rows fit.
-  while (blocks && (rc = lean_rows(ctx, grid_for(blocks * G) * kBlock, blocks * G * kBlock, chunk, &rows,
-                                   ctx->has_textures || tree, mm))) {
+  // On an allocation failure the launches shrink (G halved) until the records fit.
+  while (blocks && (rc = path_records(ctx, grid_for(blocks * G) * kBlock, blocks * G * chunk * kBlock, &rec, &anchors,
+                                      tex_rec, mm))) {
     if (G == 1 || O.groups) return rc;
     G = (G + 1) / 2;
     (void)hipGetLastError();  // clear the failed hipMalloc's error state
@@ -2700,9 +2682,15 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
     const uint32_t grid = (uint32_t)grid_for(L.nblocks);
     if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
-    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rows.lvl, rows.anchor,
-                       rows.tex, rows.rad, rows.mat, (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
-    hipLaunchKernelGGL(dev::fold_groups, dim3((uint32_t)blocks), dim3(kBlock), 0, ctx->stream, F, L, rows.rad);
+    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rec, anchors,
+                       (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
+    const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
+    auto fold = tex_rec ? (mm ? (lm ? dev::fold_paths<true, true, true> : dev::fold_paths<true, true, false>)
+                              : (lm ? dev::fold_paths<true, false, true> : dev::fold_paths<true, false, false>))
+                        : (mm ? (lm ? dev::fold_paths<false, true, true> : dev::fold_paths<false, true, false>)
+                              : (lm ? dev::fold_paths<false, false, true> : dev::fold_paths<false, false, false>));
+    hipLaunchKernelGGL(fold, dim3((uint32_t)blocks), dim3(kBlock), lm ? 48 * ctx->scene.num_materials : 0,
+                       ctx->stream, ctx->scene, F, L, rec);
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -2763,7 +2751,7 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                c.phase[10], c.phase[12], 100.0 * c.phase[12] / (64.0 * (c.phase[10] ? c.phase[10] : 1)), c.phase[11],
                c.phase[13], 100.0 * c.phase[13] / (64.0 * (c.phase[11] ? c.phase[11] : 1)));
   std::fprintf(stderr,
-               "[fs small] small-mesh faces %llu cycles (inside mesh-traversal); lanes per iteration: tracing %.1f, "
+               "[fs small] small-mesh faces %llu cycles (in trace, apart from root-cull and mesh-traversal); lanes per iteration: tracing %.1f, "
                "shading %.1f, finishing %.1f; unwind levels per finished path %.2f\n",
                c.phase[14], (double)c.phase[26] / (c.phase[8] ? c.phase[8] : 1),
                (double)c.phase[27] / (c.phase[8] ? c.phase[8] : 1), (double)c.phase[28] / (c.phase[8] ? c.phase[8] : 1),

@@ -5,10 +5,11 @@
 // scene.cpp:227-249 (closest hit + back-face flip), object.cpp / intersect.cpp
 // (primitive tests), material.cpp + normal.cpp (BRDF sampling and shading)
 // and frame.cpp:53-85 (running-mean accumulation). The recursion of TraceStep
-// is unrolled into a forward pass that stages each bounce's shading scalars
-// in per-lane HBM scratch rows (L2-resident) and a backward
-// pass that applies Material::Sample in the reference's order, so the float
-// rounding matches the recursive reference bit for bit.
+// is unrolled into a forward pass (the megakernel) that writes each bounce's
+// shading scalars and each path's end state to per-sample path records in
+// HBM, and a backward pass (fold_paths) that applies Material::Sample in the
+// reference's order and folds the samples into the frame, so the float
+// rounding matches the recursive reference bit for bit (DESIGN.md §4, §10b).
 #pragma once
 
 #include "fs_scene.h"
@@ -29,8 +30,8 @@ constexpr uint32_t kPackedMaterials = 255;
 // about one block's duration).
 constexpr uint64_t kGroupTargetBlocks = 262144;
 // Persistent launches: sample groups per launch up to this many bytes of
-// radiance rows (12 B per sample; of 288 GB of HBM).
-constexpr uint64_t kRadianceRowBytes = 32ull << 30;
+// path records (88 B per sample of an untextured scene; of 288 GB of HBM).
+constexpr uint64_t kRecordBytes = 96ull << 30;
 
 struct DevScene {
   const DevObject* __restrict__ objects;
@@ -38,6 +39,11 @@ struct DevScene {
   const DevTri* __restrict__ tris;
   const float4* __restrict__ tri_normals;
   const fs_material* __restrict__ materials;
+  // Per material the fields of the backward pass, 3 float4: (kind bits,
+  // diffuse), (roughness, emissive), (glow, texture bits); fold_paths stages
+  // them in LDS.
+  const float4* __restrict__ umat;
+  uint32_t num_materials;
   const float4* __restrict__ table;
   const float* __restrict__ tex_rgb;   // all textures, 3 floats per texel
   const uint4* __restrict__ tex_info;  // first float, width, height, 0
@@ -78,6 +84,22 @@ struct DevCounters {
   unsigned long long phase[32];
 };
 
+// The path records of one launch, indexed by sample
+// q = (the block's record row) x spp x 64 + slot, every per-level array level-major
+// ([level][q]: a wave's lanes at one depth store and fold_paths' lanes load
+// consecutive samples). The megakernel writes them; fold_paths reads them
+// once, runs the backward pass and folds the radiance into the frame.
+struct PathRecords {
+  float* c;        // [level][q]: c = max(0, n.r)
+  float* ds;       // [level][q]: Ceramic/Glow's specular term (written by those bounces only)
+  float4* end;     // [q]: the radiance entering level top + 1, and (w, as bits) top + 1 | kRecFogDif
+  uint2* mats;     // [q]: the packed 8-bit material ids of levels 0-3 and 4-7 (<= 255 materials)
+  uint32_t* mat;   // [level][q]: the material id of every level (MMAT), else null
+  float4* tex;     // [level][q]: SampleDiffuse's texel of a textured material (TEX), else null
+  uint64_t n;      // samples of the launch (the level stride)
+};
+constexpr uint32_t kRecFogDif = 0x100u;  // level 0 is Fog and its draw took the diffuse colour
+
 struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;
   uint32_t sample_base, spp;
@@ -87,15 +109,14 @@ struct Launch {
   uint32_t xcd_bands;  // 1: each XCD (blocks b, b+8, ...) renders one contiguous band of micro-tiles
   // Sample groups: one launch renders `groups` consecutive runs of `spp`
   // samples; block (g, micro-tile) takes samples sample_base + g*spp ...
-  // Groups > 1 leave the radiance rows for fold_groups, which folds them into
-  // the frame in sample order (the launch tail and a small multi-GPU share no
+  // fold_paths folds every group's path records into the frame in sample order (the launch tail and a small multi-GPU share no
   // longer leave CUs idle).
   uint32_t groups;
   uint32_t owned;  // 64x64 tiles this launch renders per group
   uint32_t group_major;  // block order: 0 a tile's groups together, 1 group by group (A/B)
   // Dispatch order of the owned tiles (owned entries of owned-tile indices),
   // or null for index order. Only the order changes: every tile keeps its
-  // radiance rows, so frames are identical.
+  // path records, so frames are identical.
   const uint32_t* tile_order;
   uint64_t seed;
   uint32_t nblocks;  // blocks of the launch: owned tiles x micro-tiles x groups

@@ -17,18 +17,17 @@ import isa_guard  # noqa: E402
 
 # kernel (as fs_last_kernel names it) -> (max scratch B/lane, max SGPR spills, VGPRs)
 LIMITS = {
-    # PARKED schedule: C3 and C4 (the bench kernel). 44 -> 60 B/lane with the
-    # lane-major rows and the unrolled backward pass (C4 +3.5 % all the same,
-    # profiles/r03/ab_lrows.log)
-    "render_kernel_lean<false, 6, false, true, false, false, false>": (60, 21, 80),
-    # LEAN schedule: scenes with BVH walks and no large mesh. 16 -> 20 B/lane
-    # without the traversal s_setprio (FS_TRAV_PRIO 0: C4 +1.1 %, C3 +0.3 % on
-    # the parked-walk kernel, profiles/r03/ab_sched.log; no bench config runs LEAN)
-    "render_kernel_lean<false, 6, false, false, false, false, false>": (20, 12, 80),
-    # LEAN without walks (NOWALK: every mesh small, shading rows in LDS, 8 waves
-    # per SIMD): C1 and C2. 32 -> 44 B/lane with the straight-line mesh-root
-    # cull on the segment's slopes (C2 +6.7 % all the same, profiles/r03/ab_root_tol.log)
-    "render_kernel_lean<false, 8, false, false, false, false, true>": (44, 27, 64),
+    # PARKED schedule: C3 and C4 (the bench kernel). 60 -> 40 B/lane once the
+    # backward pass left the kernel for fold_paths (round 4: C4 +4.5 %,
+    # profiles/r04/ab_records.log)
+    "render_kernel_lean<false, 6, false, true, false, false, false>": (40, 21, 80),
+    # LEAN schedule: scenes with BVH walks and no large mesh. 16 B/lane; SGPR
+    # spills 12 -> 14 with the backward-pass material table's pointer and count
+    # in the scene record (round 4; no bench config runs LEAN)
+    "render_kernel_lean<false, 6, false, false, false, false, false>": (16, 14, 80),
+    # LEAN without walks (NOWALK: every mesh small, no walk stack, 8 waves per
+    # SIMD): C1 and C2. 44 -> 40 B/lane without the backward pass (C2 +8.5 %)
+    "render_kernel_lean<false, 8, false, false, false, false, true>": (40, 27, 64),
 }
 
 
