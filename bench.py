@@ -62,10 +62,11 @@ S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 96, 24
 # tools/cpu_calibration.py on SURVEY Appendix A's own probe scenes (the C1 room + a UV-sphere blob,
 # scenes.write_probe), 8 threads in the build container, against the reference rates and octree
 # counts SURVEY records for them
-CPU_CALIBRATION = ("oracle vs reference on SURVEY's probe scenes (8 threads, build container, DESIGN §6): "
-                   "250k probe rate x1.40 at 3.50 vs 5.02 segments/sample and 145 vs 137 triangle tests per "
-                   "segment, i.e. x1.03 per triangle test; 1M probe x1.09 at 3.37 vs 5.05 and 483 vs 451, "
-                   "x0.78 per triangle test; the reference cannot be built here for a same-machine run")
+CPU_CALIBRATION = ("oracle vs reference on SURVEY's probe scenes (8 threads, build container, DESIGN §6, "
+                   "profiles/r04/cpu_calibration.log): 250k probe rate x1.22 at 3.52 vs 5.02 segments/sample and "
+                   "153 vs 137 triangle tests per segment, i.e. x0.96 per triangle test; 1M probe x1.11 at 3.50 vs "
+                   "5.05 and 508 vs 451, x0.87 per triangle test; the reference cannot be built here for a "
+                   "same-machine run")
 
 
 def parse():

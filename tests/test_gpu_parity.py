@@ -655,9 +655,9 @@ def test_bench_scale_parity(name, schedule, scene_dir, gpu_renderer):
 
 
 # ---- scenes with more than 255 materials (material ids in scratch rows) ----
-def many_material_scene(textured=False):
-    """A Cornell room plus 64 spheres and cuboids whose 300+ materials cycle
-    through every kind; objects use ids above 255 as well as below."""
+def many_material_scene(textured=False, n=300):
+    """A Cornell room plus 64 spheres and cuboids whose n (300+) materials
+    cycle through every kind; objects use ids above 255 as well as below."""
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
     red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
@@ -668,7 +668,7 @@ def many_material_scene(textured=False):
     kinds = [fsamd.MAT_DIFFUSE, fsamd.MAT_METAL, fsamd.MAT_CERAMIC, fsamd.MAT_GLASS, fsamd.MAT_MIRROR,
              fsamd.MAT_LIQUID, fsamd.MAT_GLOW, fsamd.MAT_LIGHT, fsamd.MAT_FOG]
     mats = []
-    for i in range(300):
+    for i in range(n):
         k = kinds[i % len(kinds)]
         c = tuple(float(v) for v in rng.uniform(0.2, 0.95, 3))
         kw = {}
@@ -682,7 +682,7 @@ def many_material_scene(textured=False):
             kw.update(texture=tex, texture_scale=1.5)
         mats.append(b.material(k, diffuse=c, roughness=float(rng.uniform(0, 1)), shininess=0.6, index=0.7,
                                reflectivity=0.2, **kw))
-    assert len(b.mats) > 300
+    assert len(b.mats) > n
     for j in range(64):
         m = mats[(37 * j + 250) % len(mats)]
         x, y, z = rng.uniform(-8, 8), rng.uniform(1, 18), rng.uniform(-8, 8)
@@ -707,6 +707,20 @@ def test_many_materials_bit_exact(variant, gpu_renderer):
     k = gpu_renderer.last_kernel()
     assert k[:-1].split(", ")[4] == "true", k  # the MMAT instantiation <.., TEX, SUSP, MMAT, SOCT, NOWALK>
     assert (k[:-1].split(", ")[3] == "true") == (variant == "parked"), k
+    ref = oracle_render(ptr, CAM, 96, 72, 16)
+    assert_parity(out, ref, exact=True)
+
+
+def test_material_table_outside_lds_bit_exact(gpu_renderer):
+    """Between 65 and 255 materials the ids stay packed in two registers but
+    fold_paths reads the backward pass's material table from global memory
+    instead of LDS (it stages at most 64): bit-exact with the oracle, every
+    kind present."""
+    b = many_material_scene(n=120)
+    ptr = b.build()
+    out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    k = gpu_renderer.last_kernel()
+    assert k[:-1].split(", ")[4] == "false", k  # packed material ids (no MMAT)
     ref = oracle_render(ptr, CAM, 96, 72, 16)
     assert_parity(out, ref, exact=True)
 

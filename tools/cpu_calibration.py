@@ -24,8 +24,9 @@ import scenes  # noqa: E402
 # the reference octree's segments per sample and triangle tests per segment
 REF_RATE = {"c1": 0.73, "probe250": 0.180, "probe1m": 0.067, "c4": 0.067}
 REF_COUNTS = {"c1": (5.1, 15.8), "probe250": (5.02, 137.0), "probe1m": (5.05, 451.0)}
-CONFIGS = (("c1", 256, 256, 8, 1), ("probe250", 1920, 1080, 1, 8), ("probe1m", 1920, 1080, 1, 16),
-           ("c4", 1920, 1080, 1, 16))
+# (name, W, H, spp, tile stride): about 5-10 s of oracle time each on 8 threads
+CONFIGS = (("c1", 256, 256, 32, 1), ("probe250", 1920, 1080, 1, 2), ("probe1m", 1920, 1080, 1, 4),
+           ("c4", 1920, 1080, 1, 4))
 
 
 def main():
@@ -59,6 +60,8 @@ def main():
         rs, rt = REF_COUNTS.get(name, (None, None))
         counts = f"segments/sample {seg:.2f} (survey {rs}), tri tests/segment {tri:.1f} (survey {rt}), " \
                  f"octree nodes/segment {node:.1f}"
+        if rs:  # the rate per triangle test, which takes the scene's path lengths out of the ratio
+            counts += f"; per triangle test x{(rate * seg * tri) / (REF_RATE[name] * rs * rt):.2f}"
         print(f"{name} {W}x{H}: {st['samples']} samples in {dt:.1f}s -> {rate:.3f} Msamples/s "
               f"(reference probe {REF_RATE[name]}; ratio {rate / REF_RATE[name]:.2f}); {counts}; "
               f"octree build {build:.1f}s", flush=True)
