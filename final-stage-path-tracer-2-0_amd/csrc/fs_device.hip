@@ -581,8 +581,9 @@ __device__ __forceinline__ bool fog_takes_diffuse(const fs_material& m, f3 p0, f
 // the radiance of level top + 1; c holds the path's c values (levels
 // <= top), M the backward-pass material table (DevScene::umat, in LDS or
 // global memory). Levels run unrolled over wave-uniform indices (each lane
-// applies the levels <= its top), and every kind is one straight-line
-// sequence of selects, each kind's operations in the reference's order:
+// applies the levels <= its top), each kind's operations in the reference's
+// order (a per-kind switch: +0.2-0.3 % over one straight-line select
+// sequence of every kind, profiles/r04/ab_fold_switch.log):
 //   Diffuse  (sd*L)*c                     Metal  ((sd*L)*c)*r + (sd*L)*(1-r)
 //   Mirror/Glass/Liquid  L*dif            Ceramic  L*ds + ((sd*L)*c)*(1-ds) (+glow)
 //   Light  emissive (its texel when mapped), Fog  L or, at level 0, dif when
@@ -608,23 +609,40 @@ __device__ __forceinline__ f3 unwind_path(MatPtr M, const PathRecords& R, uint64
         sd = mk3(tx.x, tx.y, tx.z);
       }
     }
-    const bool mirrorish = kk == FS_MAT_MIRROR || kk == FS_MAT_GLASS || kk == FS_MAT_LIQUID;
-    const bool metal = kk == FS_MAT_METAL, cer = kk == FS_MAT_CERAMIC || kk == FS_MAT_GLOW;
-    float wa = 0.0f;  // the two weights of Metal and Ceramic
-    if (metal) wa = m1.x;
-    if (cer) wa = R.ds[(uint64_t)k * R.n + q];
-    const float wb = (float)(1.0 - (double)wa);
-    const f3 t = (mirrorish ? dk : sd) * L;  // L*dif is dif*L bit for bit
-    const f3 dc = t * c[k];
-    f3 mix = (metal ? dc : L) * wa + (metal ? t : dc) * wb;
-    if (kk == FS_MAT_GLOW) {
-      const float4 m2 = M[3 * id + 2];
-      mix = mix + mk3(m2.x, m2.y, m2.z);
+    f3 out = L;
+    switch (kk) {
+      case FS_MAT_LIGHT:
+        out = (TEX && mapped) ? sd : mk3(m1.y, m1.z, m1.w);
+        break;
+      case FS_MAT_DIFFUSE:
+        out = (sd * L) * c[k];
+        break;
+      case FS_MAT_METAL: {
+        const f3 dc = (sd * L) * c[k];
+        const f3 rc = sd * L;
+        out = dc * m1.x + rc * (float)(1.0 - (double)m1.x);
+        break;
+      }
+      case FS_MAT_MIRROR:
+      case FS_MAT_GLASS:
+      case FS_MAT_LIQUID:
+        out = L * dk;
+        break;
+      case FS_MAT_CERAMIC:
+      case FS_MAT_GLOW: {
+        const float ds = R.ds[(uint64_t)k * R.n + q];
+        const f3 dc = (sd * L) * c[k];
+        out = L * ds + dc * (float)(1.0 - (double)ds);
+        if (kk == FS_MAT_GLOW) {
+          const float4 m2 = M[3 * id + 2];
+          out = out + mk3(m2.x, m2.y, m2.z);
+        }
+        break;
+      }
+      default:
+        if (k == 0 && fog_dif) out = dk;
+        break;
     }
-    f3 out = kk == FS_MAT_DIFFUSE ? dc : ((metal || cer) ? mix : (mirrorish ? t : L));
-    if (kk == FS_MAT_LIGHT)  // material.cpp:43-53
-      out = (TEX && mapped) ? sd : mk3(m1.y, m1.z, m1.w);
-    if (kk == FS_MAT_FOG && k == 0 && fog_dif) out = dk;
     L = out;
     if (k == 0) kind0 = kk;
   }
