@@ -169,10 +169,10 @@ def run(args, rank, world, local_rank, group):
             g_ms = (time.perf_counter() - tg) * 1e3
         else:
             r.synchronize()
-        return r.last_render_ms(), g_ms
+        return r.last_render_ms(), g_ms, r.last_trace_ms()
 
     for i in range(args.warmup):
-        ms, _ = step()
+        ms, _, _ = step()
         log(f"rank {rank}: warmup {i} render {ms:.1f} ms")
 
     def barrier():
@@ -181,12 +181,13 @@ def run(args, rank, world, local_rank, group):
 
     barrier()
     r.synchronize()
-    kernel_ms, gather_ms = [], []
+    kernel_ms, gather_ms, trace_ms = [], [], []
     t_start = time.perf_counter()
     for i in range(args.steps):
-        k_ms, g_ms = step()
+        k_ms, g_ms, t_ms = step()
         kernel_ms.append(k_ms)
         gather_ms.append(g_ms)
+        trace_ms.append(t_ms)
         log(f"rank {rank}: step {i} render {k_ms:.1f} ms gather {g_ms:.1f} ms")
     r.synchronize()
     barrier()
@@ -209,8 +210,9 @@ def run(args, rank, world, local_rank, group):
     r.render(cam, cf, spp=cspp, tile_offset=rank, tile_stride=world, counters=True)
     c = r.counters()
     cf.close()
-    roofline = make_roofline(args.scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp,
+    roofline = make_roofline(args.scene, W, H, spp, c, cspp, trace_ms, kernel_name, launches, launch_spp,
                              build_id())
+    roofline["render_ms_per_step"] = round(sum(kernel_ms) / len(kernel_ms), 3)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -287,6 +289,9 @@ def roofline_bound(frac_traffic, valu_issue_frac, wait_any_frac):
 
 
 def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp, build=None):
+    """kernel_ms: per timed step, the trace kernel's HIP-event time summed over
+    its launches (fs_last_trace_ms: the dominant kernel alone, without the
+    fold_paths launches that follow each one)."""
     bytes_per_sample = (S_NODE * c["node_visits"] + S_TRI * (c["tri_tests"] + c["small_tri_loads"])
                         + S_OBJ * (c["object_loads"] + c.get("lane_object_loads", 0))
                         + S_SEG * c["segments"]) / max(c["samples"], 1) + S_SAMPLE
@@ -327,7 +332,7 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(hbm_frac, 4),
             "frac_source": "algorithmic bytes (SURVEY 8d byte model x this run's device counters) per launch / "
-                           "HIP-event launch time",
+                           "the trace kernel's HIP-event launch time (fs_last_trace_ms)",
             "traffic": traffic,
             "traffic_source": src if traffic else None,
             # the same launch time against the PMC-measured bytes (FETCH x2 + WRITE per launch)

@@ -2018,6 +2018,7 @@ struct fs_context {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> kev;  // (start, end) of each trace-kernel launch of the last render
   bool have_scene = false;
   DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, umat, table, counters, pack_send, tile_order,
       pack_recv, range_io, tree, tree_objs;
@@ -2311,6 +2312,7 @@ int fs_destroy(fs_context* ctx) {
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
   ctx->rows.release();
+  for (hipEvent_t e : ctx->kev) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2700,8 +2702,16 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
     const uint32_t grid = (uint32_t)grid_for(L.nblocks);
     if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
+    const size_t ke = 2 * (ctx->last_launches - 1);
+    while (ctx->kev.size() < ke + 2) {
+      hipEvent_t e;
+      FS_HIP(hipEventCreate(&e));
+      ctx->kev.push_back(e);
+    }
+    FS_HIP(hipEventRecord(ctx->kev[ke], ctx->stream));
     hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rec, anchors,
                        (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
+    FS_HIP(hipEventRecord(ctx->kev[ke + 1], ctx->stream));
     const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
     auto fold = tex_rec ? (mm ? (lm ? dev::fold_paths<true, true, true> : dev::fold_paths<true, true, false>)
                               : (lm ? dev::fold_paths<true, false, true> : dev::fold_paths<true, false, false>))
@@ -2738,6 +2748,21 @@ int fs_last_render_ms(fs_context* ctx, float* ms) {
   if ((rc = set_device(ctx))) return rc;
   FS_HIP(hipEventSynchronize(ctx->ev1));
   FS_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+  return FS_OK;
+}
+
+int fs_last_trace_ms(fs_context* ctx, float* ms) {
+  if (!ctx || !ms) return fail(FS_ERR_INVALID, "null argument");
+  int rc;
+  if ((rc = set_device(ctx))) return rc;
+  float sum = 0.0f;
+  for (uint32_t i = 0; i < ctx->last_launches; i++) {
+    float t = 0.0f;
+    FS_HIP(hipEventSynchronize(ctx->kev[2 * i + 1]));
+    FS_HIP(hipEventElapsedTime(&t, ctx->kev[2 * i], ctx->kev[2 * i + 1]));
+    sum += t;
+  }
+  *ms = sum;
   return FS_OK;
 }
 

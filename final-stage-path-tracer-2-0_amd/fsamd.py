@@ -129,6 +129,7 @@ GPU_SYMBOLS = {
     "fs_synchronize": ([_VP], C.c_int),
     "fs_read_counters": ([_VP, C.POINTER(fs_counters)], C.c_int),
     "fs_last_render_ms": ([_VP, C.POINTER(C.c_float)], C.c_int),
+    "fs_last_trace_ms": ([_VP, C.POINTER(C.c_float)], C.c_int),
     "fs_last_kernel": ([_VP], C.c_char_p),
     "fs_last_render_launches": ([_VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
     "fs_comm_unique_id": ([C.c_char_p], C.c_int),
@@ -476,6 +477,12 @@ class Renderer:
     def last_render_ms(self):
         ms = C.c_float()
         _check(gpu_lib().fs_last_render_ms(self.ctx, C.byref(ms)), "fs_last_render_ms")
+        return ms.value
+
+    def last_trace_ms(self):
+        """The trace kernel's share of last_render_ms (its launches, without fold_paths)."""
+        ms = C.c_float()
+        _check(gpu_lib().fs_last_trace_ms(self.ctx, C.byref(ms)), "fs_last_trace_ms")
         return ms.value
 
     def last_kernel(self):

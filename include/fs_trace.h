@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 6
+#define FS_ABI_VERSION 7
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -243,10 +243,10 @@ typedef struct fs_options {
   uint32_t park_min_tris;      /* meshes whose walks may park (32768); read at upload */
   uint32_t samples_per_block;  /* 1..64 samples of a block's 8x8 pixels per launch group (16) */
   uint32_t groups;             /* sample groups per launch (0). 0 = automatic: with persist = 1
-                                  as many groups as a radiance-row budget allows (12 B per
-                                  sample of a launch, at most 32 GiB and at most half the free
-                                  device memory: C4 at 1080p x 1024 spp is one launch with
-                                  25.5 GB of rows); with persist = 0 enough groups for
+                                  as many groups as the path-record budget allows (88 B per
+                                  sample of a launch, 216 B textured; at most 96 GiB and at
+                                  most half the free device memory: C4 at 1080p x 1024 spp is
+                                  two launches of 512 spp); with persist = 0 enough groups for
                                   >= 262144 blocks per launch */
   uint32_t group_major;        /* block order: 0 a tile's groups together (0), 1 group by group */
   uint32_t tile_order;         /* 1 centre-first dispatch of owned tiles (1), 0 index order */
@@ -265,7 +265,9 @@ typedef struct fs_options {
                                   max 64); read at upload */
   uint32_t park_lanes_small;   /* PARKED: park_lanes for parkable meshes under 2^19 triangles (6) */
   uint32_t lds_rows;           /* 1: scenes without BVH walks (every mesh small, no texture) run
-                                  the NOWALK kernel, shading rows in LDS (1); 0 the LEAN kernel */
+                                  the NOWALK kernel: no walk stack, 8 waves per SIMD (1); 0 the
+                                  LEAN kernel. (The name dates from ABI 5, when that kernel also
+                                  kept its shading rows in LDS.) */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */
@@ -313,8 +315,14 @@ int fs_render(fs_context* ctx, const fs_camera* camera,
               const fs_render_params* params, fs_frame* frame);
 int fs_synchronize(fs_context* ctx);
 int fs_read_counters(fs_context* ctx, fs_counters* out); /* and zero them */
-/* Device time of the last fs_render's trace kernel(s) in ms (HIP events). */
+/* Device time of the last fs_render in ms (HIP events around all of it: the
+ * trace-kernel launches and the fold_paths launches after them). */
 int fs_last_render_ms(fs_context* ctx, float* ms);
+/* The part of it spent in the trace kernel (the forward pass, the dominant
+ * kernel; fs_last_kernel names it): the sum of HIP-event times around each of
+ * its launches, without the fold_paths launches (ABI 7). Profiling aid, no
+ * reference counterpart. */
+int fs_last_trace_ms(fs_context* ctx, float* ms);
 /* Name of the trace kernel the last fs_render launched, as rocprofv3 lists it
  * (the schedule depends on the scene: see DESIGN.md); "" before any render.
  * Profiling aid, no reference counterpart. */

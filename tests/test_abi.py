@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_abi_version_and_errors_without_device():
     lib = fsamd.gpu_lib()
-    assert lib.fs_abi_version() == 6
+    assert lib.fs_abi_version() == 7
     assert lib.fs_upload_scene(None, None) == -1  # FS_ERR_INVALID
     assert b"null" in lib.fs_last_error()
     assert lib.fs_render(None, None, None, None) == -1
