@@ -70,8 +70,11 @@ for step in "$@"; do
       done
       kern=$(python3 -c "import json; print([json.loads(l) for l in open('$d/p1.out') if l.startswith('{')][-1]['roofline']['kernel'])") \
         || fail "$step" $?
-      python3 tools/pmc_summary.py $d "$kern" $OUT/pmc_${sc}_${wh}.json "$sc ${wh} x $spp spp, one launch" \
-        $((w * h * spp)) > $d/summary.log 2>&1 || fail "$step" $? $d/summary.log
+      # counters are averaged per dispatch: normalise by the samples of one launch (the render may take several)
+      lspp=$(python3 -c "import json; print([json.loads(l) for l in open('$d/p1.out') if l.startswith('{')][-1]['roofline']['spp_per_launch'])") \
+        || fail "$step" $?
+      python3 tools/pmc_summary.py $d "$kern" $OUT/pmc_${sc}_${wh}.json "$sc ${wh} x $spp spp in launches of $lspp spp" \
+        $((w * h * lspp)) > $d/summary.log 2>&1 || fail "$step" $? $d/summary.log
       grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $OUT/pmc_${sc}_${wh}.json ;;
     ab)
       log=$OUT/ab_$(date +%H%M%S).log
