@@ -27,9 +27,9 @@
 // one triangle per wave trip, no wave priority in the walks, slab constants
 // once per segment, the integer-min exit clamp, the mesh-root cull as
 // straight-line masks with error-bound margins and a straight-line exact path,
-// lane-major HBM shading rows, object heads as one scalar load, 12-B radiance
-// records. The only remaining switch is FS_PHASE_PROF (the profiling build,
-// libfsgpu_prof.so).
+// object heads as one scalar load. The backward pass then left the megakernel
+// for fold_paths over per-sample path records. The only
+// remaining switch is FS_PHASE_PROF (the profiling build, libfsgpu_prof.so).
 
 namespace fs {
 namespace dev {
@@ -1430,7 +1430,7 @@ __device__ __forceinline__ void rebuild_hit(const DevScene& S, const Ray& r, con
 struct TaskBlock {
   uint32_t x0 = 0, y0 = 0, vx = 0, nvalid = 1;
   uint32_t total = 0, next = 0;  // tasks (in-frame pixels x spp) and the next one to hand out
-  uint32_t rad_row = 0;          // radiance row (group * owned + tile) * micro-tiles + micro-tile
+  uint32_t rad_row = 0;          // record row (group * owned + tile) * micro-tiles + micro-tile
   uint32_t sample0 = 0;          // sample index of the group's first sample
   bool aov = false;              // last group: its last sample leaves the AOV planes
 };
@@ -2597,11 +2597,11 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
   // Long renders are split into launches of sample groups of `chunk` samples
   // per pixel; the running mean lives in the frame, so the result is
-  // identical. A block takes any per-block count up to kChunk; its radiance
-  // row holds 3 x spp x 64 floats.
+  // identical. A block takes any per-block count up to kChunk; its record
+  // row holds spp x 64 path records.
   const uint32_t chunk = O.samples_per_block;
   // Schedule (every schedule produces identical frames): LEAN, the
-  // path-regeneration megakernel with the unwind scratch in HBM rows,
+  // path-regeneration megakernel writing path records,
   // while-while traversal and the wave's (pixel, sample) tasks pooled across
   // lanes; PARKED the same with walks of large meshes parked when few lanes
   // still walk. AUTO: PARKED when the scene has a mesh of >= park_min_tris

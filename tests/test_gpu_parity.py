@@ -351,7 +351,7 @@ def test_full_size_properties(scene_dir, gpu_renderer):
 
 def test_sample_groups_bit_exact(scene_dir, gpu_renderer):
     """A launch of G sample groups (G x 64 spp, folded in sample order by
-    fold_groups) gives the frame of G consecutive 64-spp launches, for any G,
+    fold_paths) gives the frame of G consecutive 64-spp launches, for any G,
     with a ragged last chunk, on a tile shard, and matches the oracle; so do
     the default 16-sample blocks."""
     r = gpu_renderer
