@@ -1712,8 +1712,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
-        R.c[depth * R.n + q] = c;
-        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) R.ds[depth * R.n + q] = ds;
+        // Path records are written once and read back only by fold_paths:
+        // non-temporal stores keep them from displacing the scene in the L2
+        // (C4 +0.4 %; non-temporal triangle loads lost 8-15 %: leaves are
+        // re-read by neighbouring rays; profiles/r04/ab_nontemporal.log).
+        __builtin_nontemporal_store(c, R.c + depth * R.n + q);
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) __builtin_nontemporal_store(ds, R.ds + depth * R.n + q);
         if (MMAT) R.mat[depth * R.n + q] = (uint32_t)mi;
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
@@ -1762,8 +1766,16 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         if (fog_takes_diffuse(m0, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), rng)) meta |= kRecFogDif;
       }
       const uint64_t q = rec_index(P, rad_row, slot);
-      R.end[q] = make_float4(L.x, L.y, L.z, __uint_as_float(meta));
-      if (!MMAT && top >= 0) R.mats[q] = make_uint2(mats.lo, mats.hi);
+      {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        v4f e = {L.x, L.y, L.z, __uint_as_float(meta)};
+        __builtin_nontemporal_store(e, reinterpret_cast<v4f*>(R.end + q));
+      }
+      if (!MMAT && top >= 0) {
+        typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+        v2u m = {mats.lo, mats.hi};
+        __builtin_nontemporal_store(m, reinterpret_cast<v2u*>(R.mats + q));
+      }
       if (COUNT) samples_done++;
       fresh = true;
     }
