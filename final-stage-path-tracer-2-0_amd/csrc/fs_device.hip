@@ -559,6 +559,29 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
   return r;
 }
 
+// A path-record store. Records are written once and read back only by
+// fold_paths: in the parked-walk kernel non-temporal stores keep them from
+// displacing the scene in the L2 (C4 +0.4 %; in the other kernels the
+// non-temporal form raised the spills, NOWALK 40 -> 68 B/lane, so they store
+// plainly; non-temporal triangle loads lost 8-15 %: leaves are re-read by
+// neighbouring rays; profiles/r04/ab_nontemporal.log).
+template <bool NT, class T>
+__device__ __forceinline__ void rec_store(T* p, T v) {
+  if constexpr (NT) {
+    if constexpr (sizeof(T) == 16) {
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(*reinterpret_cast<const v4f*>(&v), reinterpret_cast<v4f*>(p));
+    } else if constexpr (sizeof(T) == 8) {
+      typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(*reinterpret_cast<const v2u*>(&v), reinterpret_cast<v2u*>(p));
+    } else {
+      __builtin_nontemporal_store(v, p);
+    }
+  } else {
+    *p = v;
+  }
+}
+
 // The path record of sample `slot` (its low bits: s * 64 + 8 * py + px) of
 // the block whose record row is `row`.
 __device__ __forceinline__ uint64_t rec_index(const Launch& P, uint32_t row, uint32_t slot) {
@@ -1712,12 +1735,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           f3 hv = normalize(view * (float)-1.0 + refl);
           ds = pow50(dot(hv, nn));
         }
-        // Path records are written once and read back only by fold_paths:
-        // non-temporal stores keep them from displacing the scene in the L2
-        // (C4 +0.4 %; non-temporal triangle loads lost 8-15 %: leaves are
-        // re-read by neighbouring rays; profiles/r04/ab_nontemporal.log).
-        __builtin_nontemporal_store(c, R.c + depth * R.n + q);
-        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) __builtin_nontemporal_store(ds, R.ds + depth * R.n + q);
+        rec_store<SUSP>(R.c + depth * R.n + q, c);
+        if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) rec_store<SUSP>(R.ds + depth * R.n + q, ds);
         if (MMAT) R.mat[depth * R.n + q] = (uint32_t)mi;
         mats.set(depth, (uint32_t)mi);
         top = (int)depth;
@@ -1766,16 +1785,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         if (fog_takes_diffuse(m0, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), rng)) meta |= kRecFogDif;
       }
       const uint64_t q = rec_index(P, rad_row, slot);
-      {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        v4f e = {L.x, L.y, L.z, __uint_as_float(meta)};
-        __builtin_nontemporal_store(e, reinterpret_cast<v4f*>(R.end + q));
-      }
-      if (!MMAT && top >= 0) {
-        typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-        v2u m = {mats.lo, mats.hi};
-        __builtin_nontemporal_store(m, reinterpret_cast<v2u*>(R.mats + q));
-      }
+      rec_store<SUSP>(R.end + q, make_float4(L.x, L.y, L.z, __uint_as_float(meta)));
+      if (!MMAT && top >= 0) rec_store<SUSP>(R.mats + q, make_uint2(mats.lo, mats.hi));
       if (COUNT) samples_done++;
       fresh = true;
     }
