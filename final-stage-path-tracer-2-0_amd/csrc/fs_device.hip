@@ -958,8 +958,23 @@ __device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, FloatPtr 
 #ifdef FS_PHASE_PROF
 struct PhaseAcc {
   uint64_t cull = 0, trav = 0, prim = 0, small = 0;
+  // node trips of this trace call's BVH walks: the sum over meshes of the
+  // wave's largest per-lane count (walks one mesh after another, as run) and
+  // the wave's largest per-lane sum over meshes (if each lane went on to its
+  // next mesh's walk on its own)
+  uint64_t seq = 0, chain = 0;
 };
 #define FS_TICK() __builtin_readcyclecounter()
+__device__ __forceinline__ uint32_t prof_wave_max(uint32_t v) {  // over the active lanes
+  uint64_t m = __ballot(1);
+  uint32_t mx = 0;
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    mx = max(mx, (uint32_t)__builtin_amdgcn_readlane(v, l));
+    m &= m - 1;
+  }
+  return mx;
+}
 #else
 struct PhaseAcc {};
 #define FS_TICK() 0ull
@@ -1172,6 +1187,9 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
   const uint32_t live = SUSP ? (uint32_t)__popcll(__ballot(1)) : 0u;
   bool park = false;
   const Slopes sl = seg_slopes(r, zl);  // once per segment: the mesh-root culls' and the walks'
+#ifdef FS_PHASE_PROF
+  const uint32_t nodes_call0 = tally.lane_nodes;
+#endif
   for (uint32_t oi_ = 0; oi_ < S.num_objects; ++oi_) {
     const uint32_t oi = __builtin_amdgcn_readfirstlane(oi_);  // uniform by construction
     if (SUSP && (park || (resuming && (uint32_t)ws->oi > oi))) continue;
@@ -1204,9 +1222,15 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       } else if (SUSP) {
         // (a separate walk for zero-length rays, moving the per-node zl
         // branch out of the loop, measured 3-4 % slower: code size)
+#ifdef FS_PHASE_PROF
+        const uint32_t nodes0 = tally.lane_nodes;
+#endif
         if (visit)
           park = traverse_ww<COUNT, true>(S, (uint32_t)H.i0, (int32_t)oi, r, zl, h, stk, tally, ws, resume_here,
                                           H.i5 == 2 ? susp_thr : (H.i5 ? susp_thr_small : 0u), live, &sl);
+#ifdef FS_PHASE_PROF
+        pa.seq += prof_wave_max(tally.lane_nodes - nodes0);
+#endif
         if (resume_here) resuming = false;
 #ifdef FS_PHASE_PROF
         if (park) {
@@ -1293,6 +1317,9 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
     if (!park) ws->oi = -1;
     *parked = park;
   }
+#ifdef FS_PHASE_PROF
+  pa.chain += prof_wave_max(tally.lane_nodes - nodes_call0);
+#endif
 }
 
 // ---- textures (material.cpp:108-126, intersect.cpp:769-784) -------------
@@ -1600,6 +1627,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   WalkSuspend ws;
 #ifdef FS_PHASE_PROF
   uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t seqc[2] = {0, 0};  // PhaseAcc::seq / chain summed over this wave's trace calls
   // lane activity per iteration (wave-uniform sums): lanes tracing, shading, unwinding; unwind level trips
   uint64_t act[4] = {0, 0, 0, 0};
   uint64_t tk = __builtin_readcyclecounter(), t_begin = tk;
@@ -1689,6 +1717,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
       ph[6] += pa.trav;
       ph[7] += pa.prim;
       ph[10] += pa.small;
+      seqc[0] += pa.seq;
+      seqc[1] += pa.chain;
       act[0] += (uint64_t)__popcll(__ballot(1));
       act[1] += (uint64_t)__popcll(__ballot(!(SUSP && parked) && h.obj >= 0));
 #endif
@@ -1800,6 +1830,8 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   if (lane == 0) {
     for (int i = 0; i < 10; i++) atomicAdd(&counters->phase[i], (unsigned long long)ph[i]);
     atomicAdd(&counters->phase[14], (unsigned long long)ph[10]);
+    atomicAdd(&counters->phase[16], (unsigned long long)seqc[0]);
+    atomicAdd(&counters->phase[17], (unsigned long long)seqc[1]);
     for (int i = 0; i < 3; i++) atomicAdd(&counters->phase[26 + i], (unsigned long long)act[i]);
   }
   atomicAdd(&counters->phase[29], (unsigned long long)act[3]);
@@ -2822,6 +2854,10 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
                c.phase[14], (double)c.phase[26] / (c.phase[8] ? c.phase[8] : 1),
                (double)c.phase[27] / (c.phase[8] ? c.phase[8] : 1), (double)c.phase[28] / (c.phase[8] ? c.phase[8] : 1),
                (double)c.phase[29] / (c.phase[28] ? c.phase[28] : 1));
+  std::fprintf(stderr,
+               "[fs chain] walk node trips per trace call, summed: meshes one after another (wave max per mesh) %llu, "
+               "each lane on to its next mesh at once (wave max of the per-lane sum) %llu\n",
+               c.phase[16], c.phase[17]);
 #endif
   return FS_OK;
 }
