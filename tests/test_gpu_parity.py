@@ -545,6 +545,10 @@ def test_c5_2160p_shards_equal_single_gpu(scene_dir, gpu_renderer):
     r.render(cam, full, spp=spp)
     launches, launch_spp = r.last_launches()
     assert launches == 1 and launch_spp == spp, (launches, launch_spp)
+    # the trace kernel's share of the render (fs_last_trace_ms, ABI 7): the
+    # forward passes without the fold_paths launch behind them
+    render_ms, trace_ms = r.last_render_ms(), r.last_trace_ms()
+    assert 0.0 < trace_ms < render_ms, (trace_ms, render_ms)
     ref = {p: full.read(p) for p in (fsamd.PLANE_COLOR, fsamd.PLANE_COUNT, fsamd.PLANE_MATERIAL)}
     assert (ref[fsamd.PLANE_COUNT] == spp).all()
     assert np.isfinite(ref[fsamd.PLANE_COLOR]).all()
