@@ -33,17 +33,20 @@ def main():
         r.set_options(**fsamd.options_dict(fsamd.options(**opts)))
         base = None
         for n in ns:
-            times = []
+            times, trace = [], []
             for rank in range(n):
                 f.reset()
                 r.render(cam, f, spp=spp, tile_offset=rank, tile_stride=n, tile_size=ts)
                 times.append(r.last_render_ms())
+                trace.append(r.last_trace_ms())  # the trace kernel's share; the rest is fold_paths
             launches = r.last_launches()
             worst = max(times)
             rate = W * H * spp / worst / 1e3
             base = base or rate
             print(f"{name} {v} N={n}: slowest rank {worst:.1f} ms (mean {sum(times)/n:.1f}), "
-                  f"{rate:.0f} Msamples/s, efficiency {rate / base / n:.3f}, launches/rank {launches}", flush=True)
+                  f"{rate:.0f} Msamples/s, efficiency {rate / base / n:.3f}, launches/rank {launches}; "
+                  f"trace kernel mean {sum(trace)/n:.1f} ms, fold_paths mean {(sum(times) - sum(trace))/n:.1f} ms",
+                  flush=True)
     f.close()
     r.close()
 
