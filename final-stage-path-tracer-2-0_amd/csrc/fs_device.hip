@@ -1939,6 +1939,125 @@ __global__ __launch_bounds__(kBlock) void fold_paths(DevScene S, DevFrame F, Lau
   F.display[3 * pix + 2] = gamma8(mean.z);
 }
 
+// fold_paths for launches of few micro-tiles (a rank of a multi-GPU render):
+// the same backward passes and fold, with the serial per-pixel loop split
+// over lanes. Micro-tile
+// b (decode_block's tile-major order without the XCD placement or tile
+// order; group g's records are row g * micro-tiles + b) takes 2^fold_log2
+// workgroups, and each pixel 2^fold_log2 lanes: lane `sub` of a pixel
+// unwinds (unwind_path) samples sub, sub + 2^k, ... and the pixel's first
+// lane folds each step's 2^k radiances in sample order (frame.cpp:53-63),
+// so the frame is bit-identical to groups x spp consecutive TraceScene
+// calls. fs_render picks k > 0 only for launches of few micro-tiles (a rank
+// of a multi-GPU render), whose one-lane-per-pixel fold ran 1024 serial
+// steps on a quarter-full GPU.
+// The loads are pipelined across a lane's samples as in fold_paths. (A
+// separate kernel: the split's bookkeeping in fold_paths itself cost it 4-8
+// VGPRs, a wave per SIMD, and 0.2-0.5 % on one GPU.)
+template <bool TEX, bool MMAT, bool LDSM>
+__global__ __launch_bounds__(kBlock) void fold_paths_split(DevScene S, DevFrame F, Launch P, PathRecords R,
+                                                           uint32_t fold_log2) {
+  extern __shared__ float4 mat_lds[];
+  const uint32_t lane = threadIdx.x;
+  if (LDSM) {
+    for (uint32_t i = lane; i < 3 * S.num_materials; i += kBlock) mat_lds[i] = S.umat[i];
+    __syncthreads();
+  }
+  const uint32_t fk = fold_log2, fl = 1u << fk;  // lanes per pixel
+  const uint32_t b = blockIdx.x >> fk, part = blockIdx.x & (fl - 1u), tiles = gridDim.x >> fk;
+  const uint32_t sub = lane & (fl - 1u);
+  const uint32_t p = part * (kBlock >> fk) + (lane >> fk);  // pixel of the micro-tile
+  const uint32_t micro_per_side = P.tile_size / 8, micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t owned = b / micro_per_tile, micro = b % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t x = (tile % P.tiles_x) * P.tile_size + (micro % micro_per_side) * 8 + (p & 7);
+  const uint32_t y = (tile / P.tiles_x) * P.tile_size + (micro / micro_per_side) * 8 + (p >> 3);
+  if (x >= F.width || y >= F.height) return;  // a pixel's lanes leave together
+  const size_t pix = (size_t)y * F.width + x;
+  f3 mean = mk3(0, 0, 0);
+  uint32_t n = 0;
+  if (sub == 0) {
+    mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
+    n = F.count[pix];
+  }
+  const uint32_t total = P.groups * P.spp;
+  auto rec = [&](uint32_t i) {  // sample i of the pixel: group i / spp, sample i % spp
+    const uint32_t g = i / P.spp, k = i - g * P.spp;
+    return rec_index(P, g * tiles + b, k * kBlock + p);
+  };
+  auto load_c = [&](uint64_t q, int top, float (&c)[kMaxDepth]) {
+#pragma unroll
+    for (int k = 0; k < (int)kMaxDepth; k++) c[k] = k <= top ? R.c[(uint64_t)k * R.n + q] : 0.0f;
+  };
+  auto top_of = [](const float4& e) { return (int)(__float_as_uint(e.w) & 0xFFu) - 1; };
+  // this lane's samples i (a), i + fl (b), i + 2 fl (e2, m2); a lane past
+  // the last sample keeps a zero record (top -1) that is never folded
+  uint32_t i = sub;
+  uint64_t qa = 0, qb = 0;
+  float4 ea = make_float4(0, 0, 0, 0), eb = make_float4(0, 0, 0, 0);
+  uint2 ma = make_uint2(0u, 0u), mb = make_uint2(0u, 0u);
+  if (i < total) {
+    qa = rec(i);
+    ea = R.end[qa];
+    if (!MMAT) ma = R.mats[qa];
+  }
+  if (i + fl < total) {
+    qb = rec(i + fl);
+    eb = R.end[qb];
+    if (!MMAT) mb = R.mats[qb];
+  }
+  float ca[kMaxDepth], cb[kMaxDepth];
+  load_c(qa, top_of(ea), ca);
+  for (uint32_t base = 0; base < total; base += fl, i += fl) {  // base: wave-uniform
+    uint64_t q2 = qb;
+    float4 e2 = eb;
+    uint2 m2 = mb;
+    load_c(qb, top_of(eb), cb);
+    if (i + 2 * fl < total) {
+      q2 = rec(i + 2 * fl);
+      e2 = R.end[q2];
+      if (!MMAT) m2 = R.mats[q2];
+    } else {
+      e2 = make_float4(0, 0, 0, 0);
+    }
+    const uint32_t meta = __float_as_uint(ea.w);
+    f3 L;
+    if (LDSM)
+      L = unwind_path<TEX, MMAT>(static_cast<const float4*>(mat_lds), R, qa, mk3(ea.x, ea.y, ea.z), top_of(ea),
+                                 (meta & kRecFogDif) != 0, ma, ca);
+    else
+      L = unwind_path<TEX, MMAT>(S.umat, R, qa, mk3(ea.x, ea.y, ea.z), top_of(ea), (meta & kRecFogDif) != 0, ma, ca);
+    const uint32_t here = min(fl, total - base);  // samples of this step
+    {
+      for (uint32_t s = 0; s < here; s++) {  // the step's samples in order, folded by the pixel's first lane
+        const int src = (int)((lane & ~(fl - 1u)) + s);
+        const f3 Ls = mk3(__shfl(L.x, src), __shfl(L.y, src), __shfl(L.z, src));
+        if (sub == 0) {
+          f3 np = mean * (float)n + Ls;
+          float dv = (float)(++n);
+          mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+        }
+      }
+    }
+    qa = qb;
+    ea = eb;
+    ma = mb;
+#pragma unroll
+    for (int k = 0; k < (int)kMaxDepth; k++) ca[k] = cb[k];
+    qb = q2;
+    eb = e2;
+    mb = m2;
+  }
+  if (sub != 0) return;
+  F.color[3 * pix] = mean.x;
+  F.color[3 * pix + 1] = mean.y;
+  F.color[3 * pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * pix] = gamma8(mean.x);
+  F.display[3 * pix + 1] = gamma8(mean.y);
+  F.display[3 * pix + 2] = gamma8(mean.z);
+}
+
 // TraceRange (engine.cpp:298-329): one query per lane, the camera ray through
 // (x, y) without jitter or aperture, Scene::Trace, distance to the hit point.
 template <bool SOCT>
@@ -2272,6 +2391,24 @@ constexpr int kLeanWaves = 6, kSuspWaves = 6, kNowalkWaves = 8;
 // Textured scenes never park. Names as rocprofv3 prints the uncounted ones
 // (fs_last_kernel).
 typedef void (*LeanFn)(DevScene, DevCamera, DevFrame, Launch, PathRecords, float4*, uint32_t*, DevCounters*);
+typedef void (*FoldFn)(DevScene, DevFrame, Launch, PathRecords);
+typedef void (*FoldSplitFn)(DevScene, DevFrame, Launch, PathRecords, uint32_t);
+template <bool TEX, bool MMAT>
+FoldFn pick_fold2(bool lds_materials) {
+  return lds_materials ? dev::fold_paths<TEX, MMAT, true> : dev::fold_paths<TEX, MMAT, false>;
+}
+FoldFn pick_fold(bool tex, bool mmat, bool lds_materials) {
+  return tex ? (mmat ? pick_fold2<true, true>(lds_materials) : pick_fold2<true, false>(lds_materials))
+             : (mmat ? pick_fold2<false, true>(lds_materials) : pick_fold2<false, false>(lds_materials));
+}
+template <bool TEX, bool MMAT>
+FoldSplitFn pick_fold_split2(bool lds_materials) {
+  return lds_materials ? dev::fold_paths_split<TEX, MMAT, true> : dev::fold_paths_split<TEX, MMAT, false>;
+}
+FoldSplitFn pick_fold_split(bool tex, bool mmat, bool lds_materials) {
+  return tex ? (mmat ? pick_fold_split2<true, true>(lds_materials) : pick_fold_split2<true, false>(lds_materials))
+             : (mmat ? pick_fold_split2<false, true>(lds_materials) : pick_fold_split2<false, false>(lds_materials));
+}
 struct LeanKernel {
   LeanFn fn;
   const char* name;
@@ -2768,12 +2905,18 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
                        (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
     FS_HIP(hipEventRecord(ctx->kev[ke + 1], ctx->stream));
     const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
-    auto fold = tex_rec ? (mm ? (lm ? dev::fold_paths<true, true, true> : dev::fold_paths<true, true, false>)
-                              : (lm ? dev::fold_paths<true, false, true> : dev::fold_paths<true, false, false>))
-                        : (mm ? (lm ? dev::fold_paths<false, true, true> : dev::fold_paths<false, true, false>)
-                              : (lm ? dev::fold_paths<false, false, true> : dev::fold_paths<false, false, false>));
-    hipLaunchKernelGGL(fold, dim3((uint32_t)blocks), dim3(kBlock), lm ? 48 * ctx->scene.num_materials : 0,
-                       ctx->stream, ctx->scene, F, L, rec);
+    // Lanes per pixel: 1 while the launch's micro-tiles fill the chip's wave
+    // slots at least twice over, else 2 or 4 (a rank's share of a multi-GPU
+    // frame), so the serial per-pixel loop is split.
+    const uint64_t fold_slots = (uint64_t)ctx->cus * 4u * 7u;
+    const uint32_t fold_log2 = blocks >= 2 * fold_slots ? 0u : (4 * blocks >= 2 * fold_slots ? 1u : 2u);
+    const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
+    if (fold_log2 == 0)
+      hipLaunchKernelGGL(pick_fold(tex_rec, mm, lm), dim3((uint32_t)blocks), dim3(kBlock), fold_lds, ctx->stream,
+                         ctx->scene, F, L, rec);
+    else
+      hipLaunchKernelGGL(pick_fold_split(tex_rec, mm, lm), dim3((uint32_t)(blocks << fold_log2)), dim3(kBlock),
+                         fold_lds, ctx->stream, ctx->scene, F, L, rec, fold_log2);
     FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
