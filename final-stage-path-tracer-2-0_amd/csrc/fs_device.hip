@@ -2909,7 +2909,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     // slots at least twice over, else 2 or 4 (a rank's share of a multi-GPU
     // frame), so the serial per-pixel loop is split.
     const uint64_t fold_slots = (uint64_t)ctx->cus * 4u * 7u;
-    const uint32_t fold_log2 = blocks >= 2 * fold_slots ? 0u : (4 * blocks >= 2 * fold_slots ? 1u : 2u);
+    const uint32_t fold_log2 = blocks >= 2 * fold_slots ? 0u : (blocks >= fold_slots ? 1u : 2u);
     const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
     if (fold_log2 == 0)
       hipLaunchKernelGGL(pick_fold(tex_rec, mm, lm), dim3((uint32_t)blocks), dim3(kBlock), fold_lds, ctx->stream,
