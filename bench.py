@@ -43,6 +43,12 @@ fsamd.host_lib()
 METRIC = "Msamples/sec (W×H×spp/s) at 1920×1080, 1024spp; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_LANE_OPS_PEAK = 1024 * 32 * 2.4e9  # 157.3 TF FP32 vector peak / 2 (an FMA is one lane-op)
+CUS = 256
+# The scalar unit's issue ceiling, SALU instructions per CU-cycle: tools/salu_peak.hip on the
+# GPU box (profiles/r05/salu_peak.json): one CU's scalar unit issues at most one instruction
+# per cycle (0.97-0.98 over whole kernels with 24-32 waves per CU, launch and tail included;
+# one wave alone issues one every 4.7 cycles)
+SALU_PEAK_PER_CU_CYCLE = 1.0
 WORKLOADS = {
     "c4": "~1M-triangle displaced blob + Ceramic/Glass spheres + Metal cuboid in the Cornell room "
           "(BASELINE configs[3] scene; SURVEY §8d C4) at 1920x1080, 1024 spp",
@@ -274,18 +280,49 @@ def pmc_record(scene, W, H, kernel_name, build):
     return pm, path, None
 
 
-def roofline_bound(frac_traffic, valu_issue_frac, wait_any_frac):
+def roofline_bound(frac_traffic, valu_issue_frac, wait_any_frac, salu_issue_frac=None):
     """What bounds the kernel, from MEASURED fractions (the PMC summary of
-    this build): HBM when its measured traffic rate is the larger fraction of
-    its peak, VALU when the issue rate is; "latency" when neither reaches half
-    of its peak while waves wait on dependencies for more than 40 % of their
+    this build): the busiest of HBM traffic (against 8 TB/s), VALU issue
+    (against one wave64 instruction per 2 SIMD cycles) and scalar-unit issue
+    (SALU instructions per CU-cycle against the ceiling tools/salu_peak.hip
+    measured, SALU_PEAK_PER_CU_CYCLE); "latency" when none reaches half of
+    its peak while waves wait on dependencies for more than 40 % of their
     cycles. Without measurements: None (the line then says "hbm", the
     roofline frac is priced against, and bound_source says it is unmeasured)."""
     if frac_traffic is None or valu_issue_frac is None:
         return None
-    if max(frac_traffic, valu_issue_frac) < 0.5 and (wait_any_frac or 0.0) > 0.4:
+    fr = {"hbm": frac_traffic, "valu": valu_issue_frac}
+    if salu_issue_frac is not None:
+        fr["salu"] = salu_issue_frac
+    top = max(fr, key=fr.get)
+    if fr[top] < 0.5 and (wait_any_frac or 0.0) > 0.4:
         return "latency"
-    return "valu" if valu_issue_frac > frac_traffic else "hbm"
+    return top
+
+
+def bound_margins(frac_traffic, valu_issue_frac, wait_any_frac, salu_issue_frac=None, close=0.05):
+    """How firmly roofline_bound decided (a fraction near a
+    threshold flips the label on a few % of timing noise): each fraction's
+    distance to the 0.5 threshold and the wait share's to 0.4, and
+    `close_to`, the other labels roofline_bound gives when any one measured
+    input moves by +-close (5 points)."""
+    if frac_traffic is None or valu_issue_frac is None:
+        return None
+    args = [frac_traffic, valu_issue_frac, wait_any_frac, salu_issue_frac]
+    names = ["hbm", "valu", "wait", "salu"]
+    out = {f"{n}_to_{0.4 if n == 'wait' else 0.5}": round(v - (0.4 if n == "wait" else 0.5), 4)
+           for n, v in zip(names, args) if v is not None}
+    label = roofline_bound(*args)
+    alt = set()
+    for i, v in enumerate(args):
+        if v is None:
+            continue
+        for d in (-close, close):
+            moved = list(args)
+            moved[i] = v + d
+            alt.add(roofline_bound(*moved))
+    out["close_to"] = sorted(alt - {label, None})
+    return out
 
 
 def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, launch_spp, build=None):
@@ -322,14 +359,29 @@ def make_roofline(scene, W, H, spp, c, cspp, kernel_ms, kernel_name, launches, l
                 "valu_lane_op_frac": round(lane_ops / avg_launch_s / VALU_LANE_OPS_PEAK, 4),
                 "valu_insts_per_sample": pm["valu_insts_per_sample"], "clock_ghz": pm["clock_ghz"],
                 "wait_any_frac": pm.get("wait_any_frac"), "source": src}
+        if pm.get("salu_insts_per_sample"):
+            # the CU's one scalar unit: SALU instructions per CU-cycle, replayed the
+            # same way, against the ceiling tools/salu_peak.hip measured
+            salu = pm["salu_insts_per_sample"] * samples_launch / (CUS * clock * avg_launch_s)
+            valu.update({"salu_insts_per_sample": pm["salu_insts_per_sample"],
+                         "salu_per_cu_cycle": round(salu, 4),
+                         "salu_issue_frac": round(salu / SALU_PEAK_PER_CU_CYCLE, 4),
+                         "salu_peak_per_cu_cycle": SALU_PEAK_PER_CU_CYCLE})
+            if pm.get("branch_per_cu_cycle") is not None and pm.get("kernel_ms"):
+                valu["branch_per_cu_cycle"] = round(pm["branch_per_cu_cycle"] * pm["kernel_ms"] / (avg_launch_s * 1e3), 4)
+        for k in ("mean_waves_per_cu", "occupancy_pct"):  # resident waves: the kernel's, not this run's
+            if pm.get(k) is not None:
+                valu[k] = pm[k]
     frac_traffic = round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
-    bound = roofline_bound(frac_traffic, valu["valu_issue_frac"] if valu else None,
-                           valu["wait_any_frac"] if valu else None)
+    fracs = (frac_traffic, valu["valu_issue_frac"] if valu else None, valu["wait_any_frac"] if valu else None,
+             valu.get("salu_issue_frac") if valu else None)
+    bound = roofline_bound(*fracs)
     roof = {"bound": bound or "hbm",
-            "bound_source": ("measured: PMC traffic fraction, VALU issue fraction and wave wait share of this "
-                             "build (roofline_bound)") if bound else
+            "bound_source": ("measured: PMC traffic fraction, VALU and SALU issue fractions and wave wait share "
+                             "of this build (roofline_bound)") if bound else
                             f"unmeasured ({refused or 'PMC summary incomplete'}): the HBM roofline frac is priced on",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "bound_margins": bound_margins(*fracs),
             "frac": round(hbm_frac, 4),
             "frac_source": "algorithmic bytes (SURVEY 8d byte model x this run's device counters) per launch / "
                            "the trace kernel's HIP-event launch time (fs_last_trace_ms)",

@@ -784,42 +784,97 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
 // dependent per-lane node and triangle fetches.
 // A face whose plane has the previous face's bits (the two triangles of a
 // quad) reuses its plane test: intersect.cpp:728-744 on identical operands.
+// One per-lane branch per face: ray_plane's two tests (intersect.cpp:733,
+// 737) are one predicate over a quotient every lane computes, and the
+// barycentric test with the closest-hit update (intersect.cpp:357-419,
+// lower face index first among equal t) runs as selects inside the branch
+// that skips planes no lane of the wave hits. Each nested per-lane branch
+// cost the CU's one scalar unit an exec-mask save, a branch and a restore
+// per face (SALU issue 0.79 per CU-cycle on C2, against a measured ceiling
+// of about 1: tools/salu_peak.hip). The tie rule needs the face index of the
+// hit this call wrote (h.obj == oi only after a face of this call won:
+// objects are traced once per segment), kept in a register instead of
+// re-read from the hit's triangle record.
+// The closest-hit update of a small-mesh face that passed its plane test:
+// the barycentric test (intersect.cpp:146-177) and the (t, face) order, as
+// selects. (uu >= 0) && (vv >= 0) && (uu + vv <= 1): uu + vv <= 1 is
+// 1 - (uu + vv) >= 0 exactly, a NaN in uu or vv makes w NaN, and w - w is
+// NaN for a NaN or infinite w (both fail the test), else +0, which also
+// turns a -0 minimum into +0; min3 ignores NaN, the added term restores it.
+// The order (t, face) is one 64-bit key (t >= 0 here: its bits order as
+// unsigned integers once -0 becomes +0), with the best face 0 unless this
+// call wrote h (h.obj == oi only then: objects are traced once per
+// segment), so "lower face first among equal t" needs no object compare and
+// no load of the best face's record.
+__device__ __forceinline__ void small_face_hit(const TriData& T, uint32_t ti, int32_t oi, float tt, f3 pp, uint32_t point,
+                                               MinHit& h, uint32_t& bface) {
+  float uu, vv;
+  bary_pre(T, pp, uu, vv);
+  const float w = 1.0f - (uu + vv);
+  const float m = fminf(fminf(uu, vv), w) + (w - w);
+  const uint64_t key = ((uint64_t)(m >= 0.0f ? __float_as_uint(tt + 0.0f) : 0xFFFFFFFFu) << 32) | T.face;
+  const uint64_t best = ((uint64_t)__float_as_uint(h.t + 0.0f) << 32) | bface;
+  const bool better = key < best;
+  h.t = better ? tt : h.t;
+  h.obj = better ? oi : h.obj;
+  h.prim = better ? ti : h.prim;
+  h.u = better ? uu : h.u;
+  h.v = better ? vv : h.v;
+  h.point = better ? point : h.point;
+  bface = better ? T.face : bface;
+}
+// The faces of a small mesh for the lanes of non-zero-length rays.
+// ray_plane (intersect.cpp:728-744) is a hit when !cmp_eps(ts, 0) and
+// 0 <= ns / ts <= 1. cmp_eps(ts, 0, eps) is |ts| < eps (NaN: false in both),
+// and a quotient forced to -1 where it holds fails the range test, which
+// med3(q, 0, 1) == q decides (NaN: false): one compare, with no lane-mask
+// arithmetic on the scalar unit. The quotient is taken on every lane (the
+// empty asm keeps the compiler from putting the division behind a branch of
+// its own).
 template <bool COUNT>
-__device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
-                                                 const Ray& r, bool zl, MinHit& h, Tally<COUNT>& tally) {
+__device__ __forceinline__ void small_mesh_rays(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
+                                                const Ray& r, MinHit& h, Tally<COUNT>& tally) {
   bool on_plane = false;  // the plane test of the last distinct plane
   float tt = 0.0f;
   f3 pp = mk3(0, 0, 0);
+  uint32_t bface = 0;
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t ti = first + i;
     TriData T = load_tri_uniform(S.tris, ti);
     if (COUNT && threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) tally.utris++;
     if (!T.same_plane || i == 0) {  // wave-uniform
-      if (!zl) {
-        on_plane = ray_plane(T.pl, r, tt, pp);
-      } else {  // point_in_tri's plane part (intersect.cpp:320-346)
-        const float d4 = T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w * 1.0f;
-        on_plane = cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon);
-        tt = 0.0f;
-        pp = r.start;
-      }
+      const float ts = (T.pl.x * r.dir.x + T.pl.y * r.dir.y + T.pl.z * r.dir.z);
+      const float ns = -(T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w);
+      float q = ns / ts;
+      asm volatile("" : "+v"(q));
+      q = fabsf(ts) < kEpsilon ? -1.0f : q;
+      on_plane = __builtin_amdgcn_fmed3f(q, 0.0f, 1.0f) == q;
+      tt = q;
+      pp = r.start + r.dir * q;
     }
-    if (on_plane) {
-      float uu, vv;
-      bary_pre(T, pp, uu, vv);
-      if ((uu >= 0) && (vv >= 0) && (uu + vv <= 1)) {
-        bool better = tt < h.t || (tt == h.t && h.obj == oi && T.face < tri_face(S.tris, h.prim));
-        if (better) {
-          h.t = tt;
-          h.obj = oi;
-          h.prim = ti;
-          h.u = uu;
-          h.v = vv;
-          h.point = zl ? 1u : 0u;
-        }
-      }
-    }
+    if (on_plane) small_face_hit(T, ti, oi, tt, pp, 0u, h, bface);
   }
+}
+// The same for the lanes of zero-length rays (total internal reflection,
+// rare): point_in_tri (intersect.cpp:320-346), t = 0 at the segment start.
+template <bool COUNT>
+__device__ __forceinline__ void small_mesh_points(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
+                                                  const Ray& r, MinHit& h) {
+  uint32_t bface = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t ti = first + i;
+    TriData T = load_tri_uniform(S.tris, ti);
+    const float d4 = T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w * 1.0f;
+    if (cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) small_face_hit(T, ti, oi, 0.0f, r.start, 1u, h, bface);
+  }
+}
+// A lane runs the faces of its kind of ray; zero-length rays are tested in a
+// second loop that runs only when the wave holds one.
+template <bool COUNT>
+__device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
+                                                 const Ray& r, bool zl, MinHit& h, Tally<COUNT>& tally) {
+  if (!zl) small_mesh_rays<COUNT>(S, first, n, oi, r, h, tally);
+  if (__ballot(zl) && zl) small_mesh_points<COUNT>(S, first, n, oi, r, h);
 }
 
 // SUSP: when at most `thr` lanes are still walking while other live lanes of
@@ -2454,6 +2509,95 @@ bool valid_options(const fs_options* o, std::string* why) {
   return false;
 }
 
+// The record budget of a render: fs_plan_render's explicit bytes, else the
+// context's record_budget_mb, else kRecordBytes (96 GiB).
+uint64_t record_budget(const fs_options& O, uint64_t explicit_bytes) {
+  if (explicit_bytes) return explicit_bytes;
+  return O.record_budget_mb ? (uint64_t)O.record_budget_mb << 20 : kRecordBytes;
+}
+
+// How a render is cut into launches: the owned tiles in `parts` parts of at
+// most `tiles` consecutive owned tiles, each part's samples in launches of G
+// groups of `chunk` samples per block. A launch of blocks b holds
+// b x G x chunk x 64 path records. Normally one part takes every owned tile
+// and only G follows the record budget; a frame whose one-group launch
+// exceeds the budget (16K x 16K at 16 spp: 378 GB of records)
+// renders in tile parts and, below one tile per part, with fewer samples per
+// block. Tiles are disjoint and each pixel still takes its samples in order,
+// so the frame is the same.
+struct Plan {
+  uint32_t chunk = 1, G = 1, tiles = 0, parts = 0;
+  // one step smaller after an allocation failure; false when at the minimum
+  bool shrink(uint32_t owned) {
+    if (G > 1) {
+      G = (G + 1) / 2;
+    } else if (tiles > 1) {
+      tiles = (tiles + 1) / 2;
+      parts = (owned + tiles - 1) / tiles;
+    } else if (chunk > 1) {
+      chunk = (chunk + 1) / 2;
+    } else {
+      return false;
+    }
+    return true;
+  }
+  uint32_t launches(uint32_t spp) const {  // per part: the full groups, then the remainder
+    const uint32_t full = spp / chunk;
+    return parts * ((full + G - 1) / G + (spp % chunk ? 1u : 0u));
+  }
+};
+int make_plan(uint32_t owned, uint32_t mpt, uint32_t spp, const fs_options& O, uint64_t budget, size_t rec_bytes,
+              Plan* out) {
+  Plan p;
+  p.chunk = O.samples_per_block;
+  p.tiles = owned;
+  const uint64_t cap = budget / rec_bytes;          // path records one launch may hold
+  const uint64_t tile_samples = (uint64_t)mpt * kBlock;  // one sample of each pixel of one tile
+  if (owned && tile_samples * p.chunk * owned > cap) {
+    if (tile_samples > cap)
+      return fail(FS_ERR_NOMEM, "path-record budget of " + std::to_string(budget) +
+                                    " bytes is below one tile x one sample (" +
+                                    std::to_string(tile_samples * rec_bytes) + " bytes)");
+    if (tile_samples * p.chunk > cap) p.chunk = (uint32_t)(cap / tile_samples);  // >= 1
+    p.tiles = (uint32_t)std::min<uint64_t>(owned, cap / (tile_samples * p.chunk));
+  }
+  p.parts = owned ? (owned + p.tiles - 1) / p.tiles : 0;
+  // Sample groups: a launch renders G runs of `chunk` samples as G x blocks
+  // blocks, then fold_paths runs their backward passes and folds them in
+  // order. Persistent waves have a launch tail of one task path, so G is as
+  // large as the budget allows (C4 at 1080p x 1024 spp: two launches of 512
+  // spp). One-shot waves size G so a launch holds >= kGroupTargetBlocks blocks
+  // (about 43 per wave slot of the chip), within the budget.
+  const uint64_t blocks = (uint64_t)p.tiles * mpt;
+  const uint32_t full_chunks = spp / p.chunk;
+  if (blocks && full_chunks > 1) {
+    const uint64_t fit = std::max<uint64_t>(1, cap / (blocks * p.chunk * kBlock));
+    uint64_t want = O.groups    ? (uint64_t)O.groups
+                    : O.persist ? fit
+                                : std::min<uint64_t>(fit, (kGroupTargetBlocks + blocks - 1) / blocks);
+    want = std::max<uint64_t>(1, std::min<uint64_t>({want, full_chunks, ((1ull << 31) - 1) / blocks}));
+    const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
+    p.G = (full_chunks + nl - 1) / nl;                                 // balanced groups per launch
+  }
+  *out = p;
+  return FS_OK;
+}
+
+// Resident waves per CU of a fold kernel with `lds` bytes of dynamic LDS
+// (the HIP occupancy query on its compiled resources; 28 if it fails).
+uint32_t fold_waves_per_cu(const void* fn, uint32_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds) != hipSuccess || per_cu <= 0) {
+    (void)hipGetLastError();
+    return 28;
+  }
+  return (uint32_t)per_cu;
+}
+template <class Fn>
+uint32_t fold_waves_per_cu(Fn fn, uint32_t lds) {
+  return fold_waves_per_cu(reinterpret_cast<const void*>(fn), lds);
+}
+
 }  // namespace
 
 extern "C" {
@@ -2787,11 +2931,6 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   DevCamera C = camera_basis(camera, params->width, params->height);
   DevFrame F = frame_view(frame);
   bool count = (params->flags & FS_RENDER_COUNTERS) != 0;
-  // Long renders are split into launches of sample groups of `chunk` samples
-  // per pixel; the running mean lives in the frame, so the result is
-  // identical. A block takes any per-block count up to kChunk; its record
-  // row holds spp x 64 path records.
-  const uint32_t chunk = O.samples_per_block;
   // Schedule (every schedule produces identical frames): LEAN, the
   // path-regeneration megakernel writing path records,
   // while-while traversal and the wave's (pixel, sample) tasks pooled across
@@ -2803,45 +2942,56 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   if (parked && ctx->has_textures) return fail(FS_ERR_INVALID, "the PARKED schedule does not take textured scenes");
   if (parked && ctx->scene.tree)
     return fail(FS_ERR_INVALID, "the PARKED schedule does not take scenes traced through the object octree");
+  if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
   FS_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-  // Sample groups: a launch renders G runs of `chunk` samples as
-  // G x blocks blocks, then fold_paths runs their backward passes and folds
-  // them in order. Persistent waves have a launch tail of one task path, so G
-  // is as large as the path records allow (kRecordBytes: C4 at 1080p x 1024
-  // spp is two launches of 512 spp). One-shot waves size G so a launch holds
-  // >= kGroupTargetBlocks blocks (about 43 per wave slot of the chip).
-  const uint32_t full_chunks = params->spp / chunk;
-  uint32_t G = 1;
   const bool tree = ctx->scene.tree != nullptr;
   const bool mm = ctx->many_materials || tree;
   const bool tex_rec = ctx->has_textures || tree;
   const size_t rec_bytes = record_bytes(tex_rec, mm);
-  // The path records of a persistent launch: at most kRecordBytes and at
-  // most half of the device memory that is free (counting the records this
-  // context already holds), so a smaller or shared GPU renders in more,
-  // smaller launches instead of failing.
-  uint64_t row_budget = kRecordBytes;
+  // The path records of a launch: at most the record budget (96 GiB, or
+  // fs_options.record_budget_mb) and at most half of the device memory that
+  // is free (counting the records this context already holds), so a smaller
+  // or shared GPU renders in more, smaller launches instead of failing.
+  uint64_t row_budget = record_budget(O, 0);
   {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
       row_budget = std::min<uint64_t>(row_budget, (free_b + ctx->rows.bytes) / 2);
   }
-  if (blocks && full_chunks > 1) {
-    uint64_t want = O.groups  ? (uint64_t)O.groups
-                    : O.persist ? std::max<uint64_t>(1, row_budget / (blocks * rec_bytes * chunk * kBlock))
-                                : (kGroupTargetBlocks + blocks - 1) / blocks;
-    want = std::max<uint64_t>(1, std::min<uint64_t>({want, full_chunks, ((1ull << 31) - 1) / blocks}));
-    const uint32_t nl = (uint32_t)((full_chunks + want - 1) / want);  // launches for the full chunks
-    G = (full_chunks + nl - 1) / nl;                                   // balanced groups per launch
+  const uint32_t mpt = (ts / 8) * (ts / 8);  // micro-tiles per tile
+  Plan plan;
+  if ((rc = make_plan(owned, mpt, params->spp, O, row_budget, rec_bytes, &plan))) return rc;
+  ctx->last_launches = 0;
+  ctx->last_launch_spp = 0;
+  PathRecords rec;
+  float4* anchors = nullptr;
+  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr,
+                                   ctx->has_walks || !O.lds_rows);
+  // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
+  // K.waves waves per SIMD), never more than the launch has blocks.
+  const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
+  auto grid_for = [&](uint64_t nb) { return O.persist ? std::min<uint64_t>(wave_slots, nb) : nb; };
+  // On an allocation failure the launches shrink (groups per launch, then
+  // tiles per part, then samples per block, each halved) until the records fit.
+  while (blocks) {
+    const uint64_t pb = (uint64_t)plan.tiles * mpt;  // blocks of the largest part
+    if (!(rc = path_records(ctx, grid_for(pb * plan.G) * kBlock, pb * plan.G * plan.chunk * kBlock, &rec, &anchors,
+                            tex_rec, mm)))
+      break;
+    if (O.groups || !plan.shrink(owned)) return rc;
+    (void)hipGetLastError();  // clear the failed hipMalloc's error state
   }
-  L.owned = owned;
+  ctx->last_kernel = K.name;
+  L.persist = O.persist;
   L.groups = 1;
   L.group_major = O.group_major;
   L.tile_order = nullptr;
-  if (owned > 1 && O.tile_order) {
-    // Longest jobs first: tiles nearer the image centre (where the scenes put
-    // their geometry) are dispatched first, so the launch tail runs on cheap
-    // edge tiles. Ties keep index order.
+  // Longest jobs first: tiles nearer the image centre (where the scenes put
+  // their geometry) are dispatched first, so the launch tail runs on cheap
+  // edge tiles. Ties keep index order. Only the dispatch order changes: every
+  // tile keeps its path records. (A render in several tile parts dispatches
+  // each part in index order.)
+  if (owned > 1 && O.tile_order && plan.parts == 1) {
     const uint64_t key[3] = {((uint64_t)L.tile_offset << 32) | L.tile_stride, owned,
                              ((uint64_t)params->width << 32) | params->height};
     std::vector<uint32_t>& ord = ctx->tile_order_host;
@@ -2864,62 +3014,85 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     }
     L.tile_order = (const uint32_t*)ctx->tile_order.p;
   }
-  ctx->last_launches = 0;
-  ctx->last_launch_spp = 0;
-  PathRecords rec;
-  float4* anchors = nullptr;
-  const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr,
-                                   ctx->has_walks || !O.lds_rows);
-  // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
-  // K.waves waves per SIMD), never more than the launch has blocks.
-  const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
-  auto grid_for = [&](uint64_t nb) { return O.persist ? std::min<uint64_t>(wave_slots, nb) : nb; };
-  if (blocks >= (1ull << 31)) return fail(FS_ERR_INVALID, "frame too large (2^31 or more 8x8 blocks)");
-  // On an allocation failure the launches shrink (G halved) until the records fit.
-  while (blocks && (rc = path_records(ctx, grid_for(blocks * G) * kBlock, blocks * G * chunk * kBlock, &rec, &anchors,
-                                      tex_rec, mm))) {
-    if (G == 1 || O.groups) return rc;
-    G = (G + 1) / 2;
-    (void)hipGetLastError();  // clear the failed hipMalloc's error state
-  }
-  ctx->last_kernel = K.name;
-  L.persist = O.persist;
-  for (uint32_t done = 0; done < params->spp && blocks;) {
-    L.sample_base = params->sample_base + done;
-    L.spp = std::min(chunk, params->spp - done);
-    L.groups = L.spp == chunk ? std::min(G, (params->spp - done) / chunk) : 1u;
-    L.nblocks = (uint32_t)(blocks * L.groups);
-    done += L.groups * L.spp;
-    ctx->last_launches++;
-    ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
-    const uint32_t grid = (uint32_t)grid_for(L.nblocks);
-    if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
-    const size_t ke = 2 * (ctx->last_launches - 1);
-    while (ctx->kev.size() < ke + 2) {
-      hipEvent_t e;
-      FS_HIP(hipEventCreate(&e));
-      ctx->kev.push_back(e);
+  const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
+  const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
+  const FoldFn fold = pick_fold(tex_rec, mm, lm);
+  const FoldSplitFn fold_split = pick_fold_split(tex_rec, mm, lm);
+  // Lanes per pixel of the fold: 1 while a launch's micro-tiles fill the
+  // fold kernel's resident wave slots at least twice over, else 2 or 4 (a
+  // rank's share of a multi-GPU frame), so the serial per-pixel loop is split.
+  const uint64_t fold_slots = (uint64_t)ctx->cus * fold_waves_per_cu(fold, fold_lds);
+  for (uint32_t part = 0; part < plan.parts; part++) {
+    // part p: the render's owned tiles p * tiles ..., i.e. the frame's tiles
+    // tile_offset + (p * tiles + i) * stride
+    const uint32_t first = part * plan.tiles;
+    L.owned = std::min<uint32_t>(plan.tiles, owned - first);
+    L.tile_offset = params->tile_offset + first * stride;
+    const uint64_t pblocks = (uint64_t)L.owned * mpt;
+    const uint32_t fold_log2 = pblocks >= 2 * fold_slots ? 0u : (pblocks >= fold_slots ? 1u : 2u);
+    for (uint32_t done = 0; done < params->spp;) {
+      L.sample_base = params->sample_base + done;
+      L.spp = std::min(plan.chunk, params->spp - done);
+      L.groups = L.spp == plan.chunk ? std::min(plan.G, (params->spp - done) / plan.chunk) : 1u;
+      L.nblocks = (uint32_t)(pblocks * L.groups);
+      done += L.groups * L.spp;
+      const uint32_t grid = (uint32_t)grid_for(L.nblocks);
+      if (O.persist) FS_HIP(hipMemsetAsync(ctx->queues.p, 0, ctx->queues.bytes, ctx->stream));
+      const size_t ke = 2 * (size_t)ctx->last_launches;
+      while (ctx->kev.size() < ke + 2) {
+        hipEvent_t e;
+        FS_HIP(hipEventCreate(&e));
+        ctx->kev.push_back(e);
+      }
+      FS_HIP(hipEventRecord(ctx->kev[ke], ctx->stream));
+      hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rec, anchors,
+                         (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
+      FS_HIP(hipEventRecord(ctx->kev[ke + 1], ctx->stream));
+      // counted once both of its events are recorded (fs_last_trace_ms reads them)
+      ctx->last_launches++;
+      ctx->last_launch_spp = std::max(ctx->last_launch_spp, L.groups * L.spp);
+      if (fold_log2 == 0)
+        hipLaunchKernelGGL(fold, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, L, rec);
+      else
+        hipLaunchKernelGGL(fold_split, dim3((uint32_t)(pblocks << fold_log2)), dim3(kBlock), fold_lds, ctx->stream,
+                           ctx->scene, F, L, rec, fold_log2);
+      FS_HIP(hipGetLastError());
     }
-    FS_HIP(hipEventRecord(ctx->kev[ke], ctx->stream));
-    hipLaunchKernelGGL(K.fn, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->scene, C, F, L, rec, anchors,
-                       (uint32_t*)ctx->queues.p, (DevCounters*)ctx->counters.p);
-    FS_HIP(hipEventRecord(ctx->kev[ke + 1], ctx->stream));
-    const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
-    // Lanes per pixel: 1 while the launch's micro-tiles fill the chip's wave
-    // slots at least twice over, else 2 or 4 (a rank's share of a multi-GPU
-    // frame), so the serial per-pixel loop is split.
-    const uint64_t fold_slots = (uint64_t)ctx->cus * 4u * 7u;
-    const uint32_t fold_log2 = blocks >= 2 * fold_slots ? 0u : (blocks >= fold_slots ? 1u : 2u);
-    const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
-    if (fold_log2 == 0)
-      hipLaunchKernelGGL(pick_fold(tex_rec, mm, lm), dim3((uint32_t)blocks), dim3(kBlock), fold_lds, ctx->stream,
-                         ctx->scene, F, L, rec);
-    else
-      hipLaunchKernelGGL(pick_fold_split(tex_rec, mm, lm), dim3((uint32_t)(blocks << fold_log2)), dim3(kBlock),
-                         fold_lds, ctx->stream, ctx->scene, F, L, rec, fold_log2);
-    FS_HIP(hipGetLastError());
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+  return FS_OK;
+}
+
+int fs_plan_render(const fs_render_params* params, const fs_options* opt, uint64_t record_budget_bytes,
+                   uint32_t record_bytes_per_sample, fs_render_plan* out) {
+  if (!params || !out) return fail(FS_ERR_INVALID, "null argument");
+  fs_options O;
+  if (opt) {
+    std::string why;
+    if (!valid_options(opt, &why)) return fail(FS_ERR_INVALID, "fs_plan_render: " + why);
+    O = *opt;
+  } else {
+    fs_options_default(&O);
+  }
+  if (!record_bytes_per_sample) return fail(FS_ERR_INVALID, "record_bytes_per_sample must be > 0");
+  fs_frame probe;
+  probe.width = params->width;
+  probe.height = params->height;
+  uint32_t ts, stride;
+  int rc = check_params(params, &probe, &ts, &stride);
+  if (rc) return rc;
+  const uint32_t tiles = ((params->width + ts - 1) / ts) * ((params->height + ts - 1) / ts);
+  const uint32_t owned = params->tile_offset < tiles ? (tiles - params->tile_offset + stride - 1) / stride : 0;
+  const uint32_t mpt = (ts / 8) * (ts / 8);
+  Plan p;
+  if ((rc = make_plan(owned, mpt, params->spp, O, record_budget(O, record_budget_bytes), record_bytes_per_sample, &p)))
+    return rc;
+  out->parts = p.parts;
+  out->tiles_per_part = p.tiles;
+  out->samples_per_block = p.chunk;
+  out->groups_per_launch = p.G;
+  out->launches = owned ? p.launches(params->spp) : 0;
+  out->record_bytes_per_launch = (uint64_t)p.tiles * mpt * p.G * p.chunk * kBlock * record_bytes_per_sample;
   return FS_OK;
 }
 

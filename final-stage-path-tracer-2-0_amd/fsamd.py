@@ -98,7 +98,13 @@ class fs_options(C.Structure):
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
                 ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
-                ("lds_rows", C.c_uint32)]
+                ("lds_rows", C.c_uint32), ("record_budget_mb", C.c_uint32)]
+
+
+class fs_render_plan(C.Structure):
+    _fields_ = [("parts", C.c_uint32), ("tiles_per_part", C.c_uint32), ("samples_per_block", C.c_uint32),
+                ("groups_per_launch", C.c_uint32), ("launches", C.c_uint32),
+                ("record_bytes_per_launch", C.c_uint64)]
 
 
 UPLOAD_GPU_BVH = 1  # FS_UPLOAD_GPU_BVH
@@ -132,6 +138,8 @@ GPU_SYMBOLS = {
     "fs_last_trace_ms": ([_VP, C.POINTER(C.c_float)], C.c_int),
     "fs_last_kernel": ([_VP], C.c_char_p),
     "fs_last_render_launches": ([_VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
+    "fs_plan_render": ([C.POINTER(fs_render_params), C.POINTER(fs_options), C.c_uint64, C.c_uint32,
+                        C.POINTER(fs_render_plan)], C.c_int),
     "fs_comm_unique_id": ([C.c_char_p], C.c_int),
     "fs_comm_init": ([_VP, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "fs_frame_gather": ([_VP, _VP, C.POINTER(fs_render_params), C.c_int], C.c_int),
@@ -177,7 +185,7 @@ _host = None
 # Entry points added after ABI 4. A measurement build of an earlier round
 # (tools/lib_ab.sh A/B against an older libfsgpu.so, selected by
 # FSAMD_GPU_LIB) may lack them; the product library always has them.
-_OPTIONAL = {"fs_comm_count", "fs_bvh_quality"}
+_OPTIONAL = {"fs_comm_count", "fs_bvh_quality", "fs_plan_render"}
 
 
 def _bind(lib, table):

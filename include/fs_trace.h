@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 7
+#define FS_ABI_VERSION 8
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -268,6 +268,11 @@ typedef struct fs_options {
                                   the NOWALK kernel: no walk stack, 8 waves per SIMD (1); 0 the
                                   LEAN kernel. (The name dates from ABI 5, when that kernel also
                                   kept its shading rows in LDS.) */
+  uint32_t record_budget_mb;   /* path-record bytes one launch may hold, in MiB (0: 96 GiB, and
+                                  never more than half the free device memory). A frame whose
+                                  one-group launch exceeds it renders in parts of its owned tiles
+                                  and, below one tile per part, in launches of fewer samples per
+                                  block: frames are identical (ABI 8) */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */
@@ -323,6 +328,27 @@ int fs_last_render_ms(fs_context* ctx, float* ms);
  * its launches, without the fold_paths launches (ABI 7). Profiling aid, no
  * reference counterpart. */
 int fs_last_trace_ms(fs_context* ctx, float* ms);
+/* How fs_render cuts a render into launches (host only, no device needed;
+ * ABI 8): the owned tiles in `parts` parts of at most `tiles_per_part`
+ * consecutive owned tiles, each part's samples in launches of
+ * `groups_per_launch` groups of `samples_per_block` samples; `launches` in
+ * all, each holding at most `record_bytes_per_launch` bytes of path records.
+ * fs_plan_render gives the plan for a record budget of record_budget_bytes
+ * (0: opt's record_budget_mb, or 96 GiB), without the device's free-memory
+ * cap; record_bytes_per_sample is 88 for an untextured scene of <= 255
+ * materials (fs_render adds texels and material ids as the scene needs).
+ * Profiling and test aid, no reference counterpart. */
+typedef struct fs_render_plan {
+  uint32_t parts;
+  uint32_t tiles_per_part;
+  uint32_t samples_per_block;
+  uint32_t groups_per_launch;
+  uint32_t launches;
+  uint64_t record_bytes_per_launch;
+} fs_render_plan;
+int fs_plan_render(const fs_render_params* params, const fs_options* opt, uint64_t record_budget_bytes,
+                   uint32_t record_bytes_per_sample, fs_render_plan* out);
+
 /* Name of the trace kernel the last fs_render launched, as rocprofv3 lists it
  * (the schedule depends on the scene: see DESIGN.md); "" before any render.
  * Profiling aid, no reference counterpart. */

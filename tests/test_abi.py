@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_abi_version_and_errors_without_device():
     lib = fsamd.gpu_lib()
-    assert lib.fs_abi_version() == 7
+    assert lib.fs_abi_version() == 8
     assert lib.fs_upload_scene(None, None) == -1  # FS_ERR_INVALID
     assert b"null" in lib.fs_last_error()
     assert lib.fs_render(None, None, None, None) == -1
@@ -49,7 +49,7 @@ def test_options_defaults_and_validation_without_device():
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
                  "small_mesh_tris": 16, "park_lanes_small": 6,
-                 "lds_rows": 1}
+                 "lds_rows": 1, "record_budget_mb": 0}
     assert fsamd.parse_variant("schedule=parked@park_lanes=8") == {"schedule": "parked", "park_lanes": 8}
     assert fsamd.options(schedule="parked").schedule == 2
     lib = fsamd.gpu_lib()
@@ -62,6 +62,51 @@ def test_options_defaults_and_validation_without_device():
         assert lib.fs_prepare_digest(C.c_void_p(1), C.byref(ob), C.byref(d), C.byref(n), None) == -1, bad
     with pytest.raises(fsamd.FsError):
         fsamd.options(no_such_field=1)
+
+
+def _plan(width, height, spp, budget=0, rec=88, **opt):
+    lib = fsamd.gpu_lib()
+    p = fsamd.render_params(width, height, spp)
+    out = fsamd.fs_render_plan()
+    o = fsamd.options(**opt)
+    rc = lib.fs_plan_render(C.byref(p), C.byref(o), budget, rec, C.byref(out))
+    if rc:
+        raise fsamd.FsError(lib.fs_last_error().decode())
+    return out
+
+
+def test_launch_plan_of_the_bench_frame_without_device():
+    """C4 at 1080p x 1024 spp under the default 96 GiB budget: one tile part,
+    two launches of 32 groups of 16 samples."""
+    p = _plan(1920, 1080, 1024)
+    assert (p.parts, p.tiles_per_part, p.samples_per_block, p.groups_per_launch, p.launches) == (1, 510, 16, 32, 2)
+    assert p.record_bytes_per_launch <= 96 << 30
+
+
+@pytest.mark.parametrize("w,h,spp,rec,spb", [(16384, 16384, 16, 88, 16), (8192, 8192, 64, 88, 64),
+                                             (16384, 16384, 1024, 216, 16), (65536, 32768, 3, 88, 16)])
+def test_launch_plan_splits_frames_larger_than_the_budget(w, h, spp, rec, spb):
+    """a frame whose one-group launch exceeds the record budget
+    renders in tile parts (and, below one tile per part, fewer samples per
+    block) instead of failing with FS_ERR_NOMEM; every launch fits."""
+    budget = 96 << 30
+    p = _plan(w, h, spp, budget, rec, samples_per_block=spb)
+    tiles = ((w + 63) // 64) * ((h + 63) // 64)
+    assert p.parts > 1 and p.parts * p.tiles_per_part >= tiles > (p.parts - 1) * p.tiles_per_part
+    assert p.record_bytes_per_launch <= budget
+    assert p.tiles_per_part * 64 * 64 * p.samples_per_block * rec == p.record_bytes_per_launch // p.groups_per_launch
+
+
+def test_launch_plan_small_budget_without_device():
+    """record_budget_mb shrinks launches down to one tile x one sample; below
+    that the plan fails with FS_ERR_NOMEM and says why."""
+    p = _plan(256, 200, 20, 0, 88, record_budget_mb=1)  # 1 MiB: one 64x64 tile holds 360 KB per sample
+    assert (p.tiles_per_part, p.samples_per_block, p.groups_per_launch) == (1, 2, 1)
+    assert p.parts == 16 and p.launches == 16 * 10
+    p = _plan(256, 200, 20, 0, 88, record_budget_mb=128)
+    assert p.parts == 1 and p.samples_per_block == 16
+    with pytest.raises(fsamd.FsError, match="below one tile"):
+        _plan(256, 200, 20, 100000, 88)
 
 
 def test_create_fails_cleanly_without_a_gpu():

@@ -140,6 +140,27 @@ def test_roofline_bound_comes_from_measured_fractions():
     assert bench.roofline_bound(0.70, 0.33, 0.54) == "hbm"
     assert bench.roofline_bound(0.30, 0.62, 0.45) == "valu"
     assert bench.roofline_bound(None, 0.5, 0.5) is None  # unmeasured
+    # the CU's scalar unit is a port too (SQ_INSTS_SALU per CU-cycle
+    # against the ceiling tools/salu_peak.hip measured). Round 4's PMC files:
+    # C4 0.66, C2 0.79 of it, the busiest port of both
+    assert bench.roofline_bound(0.313, 0.49, 0.451, 0.66) == "salu"
+    assert bench.roofline_bound(0.09, 0.60, 0.197, 0.79) == "salu"
+    assert bench.roofline_bound(0.09, 0.60, 0.197, 0.45) == "valu"
+    assert bench.roofline_bound(0.25, 0.33, 0.54, 0.40) == "latency"
+
+
+def test_bound_margins_flag_labels_near_a_threshold():
+    """the round-4 C4 line said "latency" with VALU issue at 0.491 and
+    waits at 0.451; bound_margins reports the distances and the labels a
+    5-point move of one input would give."""
+    import bench
+
+    m = bench.bound_margins(0.313, 0.491, 0.451)
+    assert m["valu_to_0.5"] == -0.009 and m["wait_to_0.4"] == 0.051
+    assert m["close_to"] == ["valu"]
+    m = bench.bound_margins(0.09, 0.60, 0.197, 0.79)
+    assert m["close_to"] == [] and m["salu_to_0.5"] == 0.29
+    assert bench.bound_margins(None, 0.5, 0.5) is None
 
 
 def _pmc_file(root, build, kernel="render_kernel_lean<false, 6, false, true, false, false, false>"):

@@ -385,6 +385,66 @@ def test_sample_groups_bit_exact(scene_dir, gpu_renderer):
     assert_parity(frames["auto", (1, 3)][0], ref, exact=True)
 
 
+def test_record_budget_splits_into_tile_parts_bit_exact(scene_dir, gpu_renderer):
+    """a render whose one-group launch exceeds the path-record
+    budget runs in parts of its owned tiles, and below one tile per part with
+    fewer samples per block, instead of failing with FS_ERR_NOMEM. With a
+    1 MiB budget (one 64x64 tile holds 360 KB of records per sample) a 4x3-tile
+    frame renders as 12 one-tile parts of 2-sample launches; every plane equals
+    the one-launch render's, on a shard too, and matches the oracle."""
+    r = gpu_renderer
+    s = load_scene("c2", scene_dir)
+    cam = s.camera(0)
+    r.upload(s)
+    W, H, spp = 200, 136, 21  # 4x3 tiles, ragged on both edges; 10 two-sample launches + 1 per part
+    frames = {}
+    for budget in (0, 1):
+        r.set_options(record_budget_mb=budget)
+        for shard in ((0, 1), (1, 3)):
+            f = r.frame(W, H)
+            r.render(cam, f, spp=spp, tile_offset=shard[0], tile_stride=shard[1])
+            frames[budget, shard] = ({p: f.read(p) for p in range(6)}, r.last_launches())
+            f.close()
+    assert frames[0, (0, 1)][1] == (2, 16)
+    assert frames[1, (0, 1)][1] == (12 * 11, 2)
+    assert frames[1, (1, 3)][1] == (4 * 11, 2)
+    for shard in ((0, 1), (1, 3)):
+        for p in range(6):
+            np.testing.assert_array_equal(frames[1, shard][0][p], frames[0, shard][0][p], err_msg=f"{shard} plane {p}")
+    assert_parity(frames[1, (0, 1)][0], oracle_render(s.desc_ptr(), cam, W, H, spp), exact=True)
+
+
+def test_split_fold_shards_equal_single_gpu(scene_dir, gpu_renderer):
+    """a rank's share of few micro-tiles folds with 2 or 4 lanes per
+    pixel (fold_paths_split, fold_log2 1 or 2, chosen against the fold
+    kernel's resident wave slots). Shards of 1080p for tile strides 2 to 16
+    put the share on both sides of each threshold for any fold occupancy of
+    4-32 waves per CU; the union of every stride's shards is the 1-GPU frame
+    bit for bit."""
+    r = gpu_renderer
+    s = load_scene("c2", scene_dir)
+    cam = s.camera(0)
+    r.upload(s)
+    W, H, spp = 1920, 1080, 4
+    planes = (fsamd.PLANE_COLOR, fsamd.PLANE_COUNT, fsamd.PLANE_DISPLAY, fsamd.PLANE_MATERIAL)
+    full = r.frame(W, H)
+    r.render(cam, full, spp=spp)
+    ref = {p: full.read(p) for p in planes}
+    full.close()
+    part = r.frame(W, H)
+    for stride in (2, 3, 4, 5, 8, 16):
+        got = {p: np.zeros_like(v) for p, v in ref.items()}
+        for k in range(stride):
+            part.reset()
+            r.render(cam, part, spp=spp, tile_offset=k, tile_stride=stride)
+            own = part.read(fsamd.PLANE_COUNT) > 0
+            for p in got:
+                got[p][own] = part.read(p)[own]
+        for p in got:
+            np.testing.assert_array_equal(got[p], ref[p], err_msg=f"stride {stride} plane {p}")
+    part.close()
+
+
 def test_tile_sizes_cover_frame(scene_dir, gpu_renderer):
     r = gpu_renderer
     s = load_scene("c1", scene_dir)

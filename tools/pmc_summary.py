@@ -9,15 +9,12 @@ counted by both, so this is L2-miss (fabric) traffic, an upper bound on HBM.
 """
 import csv
 import glob
-import hashlib
 import json
 import os
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tools"))
-import isa_guard  # noqa: E402
 
 
 def kernel_durations(pmc_dir, kname):
@@ -28,6 +25,55 @@ def kernel_durations(pmc_dir, kname):
             if kname in row["Kernel_Name"]:
                 d.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
     return sum(d) / len(d) if d else None
+
+
+def run_build(pmc_dir):
+    """The code-object digest every profiled pass reported (its bench line's
+    roofline.build, written to p<i>.out); the passes must agree."""
+    builds = {}
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "p*.out"))):
+        lines = [json.loads(x) for x in open(f) if x.startswith("{")]
+        if not lines or not (lines[-1].get("roofline") or {}).get("build"):
+            raise SystemExit(f"{f}: no bench line with roofline.build")
+        builds[os.path.basename(f)] = lines[-1]["roofline"]["build"]
+    if not builds:
+        raise SystemExit(f"no p*.out bench lines under {pmc_dir}")
+    if len(set(builds.values())) != 1:
+        raise SystemExit(f"PMC passes ran different builds: {builds}")
+    return next(iter(builds.values()))
+
+
+# The scalar unit's issue ceiling, measured by tools/salu_peak.hip on the GPU box
+# (profiles/r05/salu_peak.json): independent scalar ALU instructions per CU-cycle
+# with every wave slot of the render kernels occupied.
+SALU_PEAK_PER_CU_CYCLE = 1.0
+
+
+def issue_fields(avg, cus=256):
+    """Per-CU-cycle issue rates of the kernel from per-dispatch counters:
+    scalar ALU (SQ_INSTS_SALU), branch (SQ_INSTS_BRANCH) and wave64 VALU
+    instructions over 256 CUs x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs),
+    the scalar rate against the measured scalar-unit ceiling, and the mean
+    resident waves per CU (SQ_WAVE_CYCLES counts quad-cycles: x4) against the
+    32 wave slots of a CU."""
+    if "GRBM_GUI_ACTIVE" not in avg:
+        return {}
+    cu_cycles = cus * avg["GRBM_GUI_ACTIVE"] / 8
+    out = {}
+    if "SQ_INSTS_SALU" in avg:
+        out["salu_per_cu_cycle"] = round(avg["SQ_INSTS_SALU"] / cu_cycles, 4)
+        if SALU_PEAK_PER_CU_CYCLE:
+            out["salu_issue_frac"] = round(out["salu_per_cu_cycle"] / SALU_PEAK_PER_CU_CYCLE, 4)
+            out["salu_peak_per_cu_cycle"] = SALU_PEAK_PER_CU_CYCLE
+    if "SQ_INSTS_BRANCH" in avg:
+        out["branch_per_cu_cycle"] = round(avg["SQ_INSTS_BRANCH"] / cu_cycles, 4)
+    if "SQ_INSTS_VALU" in avg:
+        out["valu_per_cu_cycle"] = round(avg["SQ_INSTS_VALU"] / cu_cycles, 4)
+    if "SQ_WAVE_CYCLES" in avg:
+        waves = 4 * avg["SQ_WAVE_CYCLES"] / cu_cycles
+        out["mean_waves_per_cu"] = round(waves, 2)
+        out["occupancy_pct"] = round(100 * waves / 32, 2)
+    return out
 
 
 def main():
@@ -50,9 +96,10 @@ def main():
     avg = {c: sum(d.values()) / len(d) for c, d in vals.items()}
     res = dict(meta)
     # the build the counters belong to: bench.py replays this summary only onto
-    # a run of the same code object (bench.build_id)
-    lib = os.environ.get("FSAMD_GPU_LIB") or os.path.join(ROOT, "final-stage-path-tracer-2-0_amd", "libfsgpu.so")
-    res["code_object_sha256"] = hashlib.sha256(isa_guard.code_object(lib)).hexdigest()
+    # a run of the same code object (bench.build_id). Taken from the profiled
+    # runs' own bench lines (roofline.build), not from the library on disk now,
+    # so a summary of old counters is never stamped with a later build.
+    res["code_object_sha256"] = run_build(pmc_dir)
     res["dispatches"] = {c: len(d) for c, d in vals.items()}
     res["counters_avg_per_dispatch"] = {c: round(v, 3) for c, v in sorted(avg.items())}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
@@ -92,6 +139,7 @@ def main():
             # VALU issue against its peak: a wave64 FP32 instruction every 2 cycles per SIMD
             # (MI355X_MICROARCH.md: v_fma_f32 wave64 2 cyc; = 157.3 TF FP32 at full lanes)
             res["valu_issue_frac"] = round(avg["SQ_INSTS_VALU"] * 2 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8), 4)
+    res.update(issue_fields(avg))
     res["method"] = ("rocprofv3 --pmc, one counter group per pass (tools/gpu_pmc.sh); FETCH_SIZE KiB x1024 x2 "
                      "(gfx950 half-count, MI355X_MICROARCH.md §HBM) + WRITE_SIZE KiB x1024; per dispatch average")
     if note:
