@@ -38,6 +38,16 @@ def main():
     ref = o.render(cam, fsamd.render_params(W, H, spp), threads=16)
     bad = np.argwhere((g != ref.color).any(axis=-1))
     print(f"{name} {W}x{H}x{spp}: {len(bad)} pixels differ", flush=True)
+    # every plane of the frame (frame.h:49-92), differing pixels per plane
+    planes = {"color": (fsamd.PLANE_COLOR, ref.color), "count": (fsamd.PLANE_COUNT, ref.count),
+              "display": (fsamd.PLANE_DISPLAY, ref.display), "normal": (fsamd.PLANE_NORMAL, ref.normal),
+              "depth": (fsamd.PLANE_DEPTH, ref.depth), "material": (fsamd.PLANE_MATERIAL, ref.material)}
+    per_plane = {}
+    for pname, (pid, rv) in planes.items():
+        gv = f.read(pid)
+        d = gv != rv
+        per_plane[pname] = int((d.any(axis=-1) if d.ndim == 3 else d).sum())
+    print(f"differing pixels per plane: {json.dumps(per_plane)} of {W * H}", flush=True)
     flips = []
     one = r.frame(W, H)
     per_k = {}
@@ -56,6 +66,7 @@ def main():
                 flips.append(rec)
                 print(json.dumps(rec), flush=True)
     json.dump({"scene": name, "W": W, "H": H, "spp": spp, "variant": variant, "pixels": len(bad),
+               "differing_pixels_per_plane": per_plane,
                "flips": flips}, open(out_path, "w"), indent=1)
 
 
