@@ -438,49 +438,32 @@ __device__ __forceinline__ float pow50(float xf) {
   return (float)(x32 * x16 * x2);
 }
 
-// Material::Reflection (material.cpp). The kinds that scatter around a
-// table normal (Diffuse, Metal, Glass's reflection, Ceramic, Glow) differ
-// only in the solid angle: the per-kind switch picks it, with each kind's
-// own RNG draws in their order, and the lanes of a mixed wave then run ONE
-// random_reflection together instead of one copy per kind.
-__device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, f3 view, f3 n, uint64_t& rng) {
-  enum { kScatter, kZero, kMirror, kRefract, kFrosted, kView };
-  int mode = kScatter;
-  float solid = kPi;
-  switch (m.kind) {
-    case FS_MAT_LIGHT:
-      mode = kZero;
-      break;
-    case FS_MAT_DIFFUSE:
-      break;
-    case FS_MAT_METAL:
-      solid = kPi * m.roughness;
-      break;
-    case FS_MAT_MIRROR:
-      mode = kMirror;
-      break;
-    case FS_MAT_GLASS:
-      if (rng_float(rng) < m.reflectivity)
-        solid = kPi * m.frost;
-      else
-        mode = kFrosted;
-      break;
-    case FS_MAT_LIQUID:
-      mode = rng_float(rng) < m.reflectivity ? kMirror : kRefract;
-      break;
-    case FS_MAT_CERAMIC:
-    case FS_MAT_GLOW:
-      solid = rng_float(rng) < 0.1f ? 0.0f : (float)((double)kPi * (1.0 - (double)m.shininess));
-      break;
-    default:  // FS_MAT_FOG
-      mode = kView;
-      break;
-  }
-  if (mode == kScatter) return random_reflection(S, view, n, solid, rng);
-  if (mode == kMirror) return reflect(view, n);
-  if (mode == kRefract) return refract(view, n, m.index);
-  if (mode == kFrosted) return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
-  if (mode == kView) return view;
+// Material::Reflection (material.cpp:28-339). Each kind either scatters
+// around a table normal with its solid angle (Diffuse pi, Metal pi *
+// roughness, Glass pi * frost on reflection, Ceramic and Glow 0 or
+// pi * (1 - shininess)), mirrors, refracts, refracts frosted, passes the
+// view on (Fog) or returns zero (Light); Glass, Liquid, Ceramic and Glow
+// first draw one uniform number and pick between two of these. The host
+// precomputes per material the threshold of that draw, both choices and
+// their solid angles with the reference's float / double operations
+// (DevScene::rmat), so the per-lane kind switch is one 16-B load, a draw on
+// the lanes whose material draws, and two selects; the lanes of a mixed
+// wave then run ONE random_reflection together, with each kind's RNG draws
+// in their order.
+__device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, uint32_t mi, f3 view, f3 n,
+                                             uint64_t& rng) {
+  const float4 rm = S.rmat[mi];
+  const uint32_t bits = __float_as_uint(rm.w);
+  float u = 0.0f;
+  if (bits & kReflDraws) u = rng_float(rng);
+  const bool a = u < rm.x;
+  const uint32_t mode = a ? (bits & 0xFu) : ((bits >> 4) & 0xFu);
+  const float solid = a ? rm.y : rm.z;
+  if (mode == kReflScatter) return random_reflection(S, view, n, solid, rng);
+  if (mode == kReflMirror) return reflect(view, n);
+  if (mode == kReflRefract) return refract(view, n, m.index);
+  if (mode == kReflFrosted) return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
+  if (mode == kReflView) return view;
   return mk3(0, 0, 0);
 }
 __device__ __forceinline__ bool mat_will_use(const fs_material& m, f3 r, f3 n) {
@@ -899,10 +882,21 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
   float tmax_lim = fminf(h.t, 1.0f) * 1.000002f + 1e-7f;  // h.t only changes in the leaf tests
   bool susp = false;
   while ((w != kNone || leaf) && !(SUSP && susp)) {
-    while (!(w & kLeafBit) && w != kNone) {
+    // The node loop. Its exits are wave-uniform (ballots), so the compiler
+    // keeps no per-lane exit masks across trips: a lane whose w is an inner
+    // node (w < kNone: leaf words have bit 31 set) takes the trip, the others
+    // sit it out under one exec-mask region.
+    for (;;) {
+      const bool inner = w < kNone;
+      const uint64_t walking = __ballot(inner);
+      if (!walking) break;
+      if (inner) {
       const float4* q = reinterpret_cast<const float4*>(S.nodes + w);
       float4 X = q[0], Y = q[1], Z = q[2];
       uint4 Cw = reinterpret_cast<const uint4*>(q)[3];
+      // the stack's two top entries, read while the node is in flight (slot 0
+      // stands in below the bottom of the stack; its value is not used then)
+      const uint32_t top1 = stk[(sp > 0 ? sp - 1 : 0u) * kBlock], top2 = stk[(sp > 1 ? sp - 2 : 0u) * kBlock];
       if (COUNT) tally.nodes++;
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.node_trips);
@@ -931,28 +925,38 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
         t0 = n0;
         t1 = n1;
       }
-      if (h0 && h1) {
-        bool swap = t1 < t0;
-        stk[sp * kBlock] = swap ? Cw.x : Cw.y;
-        sp++;
-        w = swap ? Cw.y : Cw.x;
-      } else if (h0 || h1) {
-        w = h0 ? Cw.x : Cw.y;
-      } else {
-        w = sp ? stk[--sp * kBlock] : kNone;
+      // The step to the next node as selects, not branches: each per-lane
+      // branch of the push / pop / park transitions cost the CU's one scalar
+      // unit an exec-mask save, a branch and a restore per node trip, on the
+      // critical path of the walking wave (a wave issues one scalar
+      // instruction per 4.7 cycles: tools/salu_peak.hip). Both children hit:
+      // go to the nearer, push the farther; one hit: go to it; none: pop.
+      // A miss enters past every hit (kMissT), so one compare orders them.
+      constexpr float kMissT = 3.0e38f;
+      const float e0 = h0 ? t0 : kMissT, e1 = h1 ? t1 : kMissT;
+      const bool swap = e1 < e0;
+      const uint32_t near = swap ? Cw.y : Cw.x, far = swap ? Cw.x : Cw.y;
+      const bool any = (swap ? e1 : e0) < kMissT, both = (swap ? e0 : e1) < kMissT;
+      stk[sp * kBlock] = far;  // a push only when both are hit (sp + 1 below); else above the top
+      const uint32_t w1 = any ? near : (sp > 0 ? top1 : kNone);
+      const uint32_t sp1 = both ? sp + 1 : (any ? sp : (sp > 0 ? sp - 1 : 0u));
+      // Park the first leaf and keep walking from the entry under it: far
+      // when both were hit, the old top after a one-child step, the one
+      // below it after a pop (read before the node arrived, like top1).
+      const bool park = (int32_t)(leaf == 0 ? w1 : 0u) < 0;  // a leaf word has bit 31 set
+      const uint32_t under = both ? far : (any ? (sp > 0 ? top1 : kNone) : (sp > 1 ? top2 : kNone));
+      leaf = park ? w1 : leaf;
+      w = park ? under : w1;
+      sp = park ? (both ? sp : (sp1 > 0 ? sp1 - 1 : 0u)) : sp1;
       }
-      if ((w & kLeafBit) && !leaf) {  // park the first leaf, keep walking
-        leaf = w;
-        w = sp ? stk[--sp * kBlock] : kNone;
-      }
-      if (__ballot(leaf == 0) == 0) break;  // every active lane holds a leaf
+      if (__ballot(inner && leaf == 0) == 0) break;  // every walking lane holds a leaf
       // Checked on every node trip: the walkers park as soon as they are few
       // (every 8th trip: C4 -9 %; every 2nd: -2 %; the trips between the drop
       // and the check ran with a nearly idle wave).
       if (SUSP) {
-        const uint32_t walkers = (uint32_t)__popcll(__builtin_amdgcn_read_exec());
+        const uint32_t walkers = (uint32_t)__popcll(walking);
         if (walkers <= thr && walkers < (uint32_t)__builtin_amdgcn_readfirstlane(live)) {
-          susp = true;
+          susp = inner;  // the lanes that took this trip park
           break;
         }
       }
@@ -1813,7 +1817,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         }
         int32_t kind = m.kind;
         f3 view = normalize(p - r.start);
-        f3 refl = mat_reflection(S, m, view, nn, rng);
+        f3 refl = mat_reflection(S, m, (uint32_t)mi, view, nn, rng);
         float c = fmaxf(0.0f, dot(nn, refl));
         float ds = 0.0f;
         if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {
@@ -2249,7 +2253,8 @@ struct fs_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> kev;  // (start, end) of each trace-kernel launch of the last render
   bool have_scene = false;
-  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, umat, table, counters, pack_send, tile_order,
+  DevBuf objects, nodes, tris, tri_normals, tri_tex, tex_rgb, tex_info, materials, umat, rmat, table, counters, pack_send,
+      tile_order,
       pack_recv, range_io, tree, tree_objs;
   fs_options opt{};  // fs_set_options; fs_options_default() at fs_create
   bool has_textures = false;
@@ -2644,7 +2649,7 @@ int fs_destroy(fs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
-                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->umat, &ctx->table, &ctx->range_io,
+                    &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->umat, &ctx->rmat, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
     b->release();
   ctx->rows.release();
@@ -2743,6 +2748,37 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
       um[3 * i + 2] = make_float4(m.glow[0], m.glow[1], m.glow[2], __int_as_float(m.texture));
     }
     if ((rc = upload(ctx, &ctx->umat, um.data(), um.size() * sizeof(float4)))) return rc;
+    // Material::Reflection's choices (DevScene::rmat, mat_reflection), each
+    // solid angle with the reference's operations: float pi * roughness and
+    // pi * frost (material.cpp:145, 199), double pi * (1 - shininess) to
+    // float (material.cpp:259-265); the draw's threshold: reflectivity
+    // (Glass, Liquid: material.cpp:197, 228) or 0.1f (Ceramic, Glow:
+    // material.cpp:259); a non-drawing kind takes choice A (0 < 1).
+    std::vector<float4> rm(P.materials.size());
+    for (size_t i = 0; i < P.materials.size(); i++) {
+      const fs_material& m = P.materials[i];
+      uint32_t a = kReflScatter, b = kReflScatter, draws = 0;
+      float thr = 1.0f, sa = kPi, sb = 0.0f;
+      switch (m.kind) {
+        case FS_MAT_LIGHT: a = kReflZero; break;
+        case FS_MAT_DIFFUSE: break;
+        case FS_MAT_METAL: sa = kPi * m.roughness; break;
+        case FS_MAT_MIRROR: a = kReflMirror; break;
+        case FS_MAT_GLASS: draws = kReflDraws; thr = m.reflectivity; sa = kPi * m.frost; b = kReflFrosted; break;
+        case FS_MAT_LIQUID: draws = kReflDraws; thr = m.reflectivity; a = kReflMirror; b = kReflRefract; break;
+        case FS_MAT_CERAMIC:
+        case FS_MAT_GLOW:
+          draws = kReflDraws;
+          thr = 0.1f;
+          sa = 0.0f;
+          sb = (float)((double)kPi * (1.0 - (double)m.shininess));
+          break;
+        default: a = kReflView; break;  // FS_MAT_FOG
+      }
+      const uint32_t w = a | (b << 4) | draws;
+      rm[i] = make_float4(thr, sa, sb, __int_as_float((int32_t)w));
+    }
+    if ((rc = upload(ctx, &ctx->rmat, rm.data(), rm.size() * sizeof(float4)))) return rc;
   }
   if ((rc = upload(ctx, &ctx->table, P.table.data(), P.table.size() * sizeof(float)))) return rc;
   if ((rc = upload(ctx, &ctx->tree, &P.tree, P.tree_valid ? sizeof(DevSceneTree) : 0))) return rc;
@@ -2783,6 +2819,7 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   S.tri_normals = (const float4*)ctx->tri_normals.p;
   S.materials = (const fs_material*)ctx->materials.p;
   S.umat = (const float4*)ctx->umat.p;
+  S.rmat = (const float4*)ctx->rmat.p;
   S.num_materials = (uint32_t)P.materials.size();
   S.table = (const float4*)ctx->table.p;
   S.tri_tex = (const float2*)ctx->tri_tex.p;

@@ -43,6 +43,10 @@ struct DevScene {
   // diffuse), (roughness, emissive), (glow, texture bits); fold_paths stages
   // them in LDS.
   const float4* __restrict__ umat;
+  // Per material Material::Reflection's choice (material.cpp), precomputed
+  // on the host: (threshold of its one uniform draw, solid angle A, solid
+  // angle B, modes and draw flag as bits; see kReflDraws): mat_reflection.
+  const float4* __restrict__ rmat;
   uint32_t num_materials;
   const float4* __restrict__ table;
   const float* __restrict__ tex_rgb;   // all textures, 3 floats per texel
@@ -98,7 +102,11 @@ struct PathRecords {
   float4* tex;     // [level][q]: SampleDiffuse's texel of a textured material (TEX), else null
   uint64_t n;      // samples of the launch (the level stride)
 };
-constexpr uint32_t kRecFogDif = 0x100u;  // level 0 is Fog and its draw took the diffuse colour
+constexpr uint32_t kRecFogDif = 0x100u;
+// DevScene::rmat.w bits: mode A (bits 0-3), mode B (bits 4-7), and whether
+// the material draws one uniform number first (Glass, Liquid, Ceramic, Glow).
+enum ReflMode : uint32_t { kReflScatter = 0, kReflZero = 1, kReflMirror = 2, kReflRefract = 3, kReflFrosted = 4, kReflView = 5 };
+constexpr uint32_t kReflDraws = 0x100u;  // level 0 is Fog and its draw took the diffuse colour
 
 struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;
