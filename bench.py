@@ -63,7 +63,7 @@ WORKLOADS = {
 # the 64-B triangle records of small meshes (fs_options.small_mesh_tris); per segment
 # one material record (76 B) + one normal-table entry (16 B) + the 4-B c value
 # its bounce writes to the path record; per sample the path record's end state
-# (16 B) and packed material ids (8 B), which fold_paths reads back (DESIGN §10b).
+# (16 B) and packed material ids (8 B), which fold_paths reads back (DESIGN §5).
 S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 96, 24
 # tools/cpu_calibration.py on SURVEY Appendix A's own probe scenes (the C1 room + a UV-sphere blob,
 # scenes.write_probe), 8 threads in the build container, against the reference rates and octree

@@ -23,12 +23,12 @@
 #include "fs_trace.h"
 
 // Round 4 pruned the compile-time A/B switches of rounds 1-3 to the settings
-// that ship (each one's measurement is in DESIGN.md §5 and §9): leaves tested
+// that ship (each one's measurement is in DESIGN_HISTORY.md §5 and §9): leaves tested
 // one triangle per wave trip, no wave priority in the walks, slab constants
 // once per segment, the integer-min exit clamp, the mesh-root cull as
 // straight-line masks with error-bound margins and a straight-line exact path,
 // object heads as one scalar load. The backward pass then left the megakernel
-// for fold_paths over per-sample path records. The only
+// for fold_paths over per-sample path records (DESIGN_HISTORY.md §10b). The only
 // remaining switch is FS_PHASE_PROF (the profiling build, libfsgpu_prof.so).
 
 namespace fs {
@@ -725,11 +725,26 @@ struct WalkSuspend {
 // closest-hit update, lower face index first among equal t.
 __device__ __forceinline__ void tri_candidate(const DevScene& S, const TriData& T, uint32_t ti, int32_t oi,
                                               const Ray& r, bool zl, MinHit& h) {
-  float t, u, v;
-  bool hit;
+  float t = 0.0f, u = 0.0f, v = 0.0f;
+  bool hit = false;
   if (!zl) {
-    f3 p;
-    hit = ray_tri(T, r, t, p, u, v);
+    // ray_tri (intersect.cpp:357-419) with ray_plane's two tests as one
+    // predicate over a quotient every lane computes (as small_mesh_rays):
+    // cmp_eps(ts, 0, eps) is |ts| < eps, a quotient forced to -1 there fails
+    // 0 <= q <= 1, which med3(q, 0, 1) == q decides (NaN: false)
+    const float ts = (T.pl.x * r.dir.x + T.pl.y * r.dir.y + T.pl.z * r.dir.z);
+    const float ns = -(T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w);
+    float q = ns / ts;
+    asm volatile("" : "+v"(q));
+    q = fabsf(ts) < kEpsilon ? -1.0f : q;
+    if (__builtin_amdgcn_fmed3f(q, 0.0f, 1.0f) == q) {
+      float uu, vv;
+      bary_pre(T, r.start + r.dir * q, uu, vv);
+      hit = (uu >= 0) && (vv >= 0) && (uu + vv <= 1);
+      t = q;
+      u = uu;
+      v = vv;
+    }
   } else {
     hit = point_in_tri(T, r.start, u, v);
     t = 0.0f;

@@ -9,7 +9,7 @@
 // shading scalars and each path's end state to per-sample path records in
 // HBM, and a backward pass (fold_paths) that applies Material::Sample in the
 // reference's order and folds the samples into the frame, so the float
-// rounding matches the recursive reference bit for bit (DESIGN.md §4, §10b).
+// rounding matches the recursive reference bit for bit (DESIGN.md §4, §5).
 #pragma once
 
 #include "fs_scene.h"
@@ -88,7 +88,7 @@ struct DevCounters {
   unsigned long long phase[32];
 };
 
-// The path records of one launch (DESIGN.md §10b), indexed by sample
+// The path records of one launch (DESIGN.md §4), indexed by sample
 // q = (the block's record row) x spp x 64 + slot, every per-level array level-major
 // ([level][q]: a wave's lanes at one depth store and fold_paths' lanes load
 // consecutive samples). The megakernel writes them; fold_paths reads them

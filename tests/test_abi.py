@@ -77,7 +77,7 @@ def _plan(width, height, spp, budget=0, rec=88, **opt):
 
 def test_launch_plan_of_the_bench_frame_without_device():
     """C4 at 1080p x 1024 spp under the default 96 GiB budget: one tile part,
-    two launches of 32 groups of 16 samples (DESIGN §10b)."""
+    two launches of 32 groups of 16 samples (DESIGN §5)."""
     p = _plan(1920, 1080, 1024)
     assert (p.parts, p.tiles_per_part, p.samples_per_block, p.groups_per_launch, p.launches) == (1, 510, 16, 32, 2)
     assert p.record_bytes_per_launch <= 96 << 30

@@ -153,6 +153,47 @@ def test_material_and_object_zoo_bit_exact(schedule, gpu_renderer):
     assert_parity(out, ref, exact=True)
 
 
+def ties_scene():
+    """A mesh whose faces tie: two coplanar copies of one triangle with
+    different vertex normals (an exact tie in t, which the lower face index
+    wins: the octree leaf tests faces in index order, intersect.cpp:357-419 and
+    mesh.cpp:277-322), listed higher-index first among the mesh's faces, a
+    needle face of near-zero area, and a face edge-on to the camera, in the
+    Cornell room (10 faces: a small mesh by default)."""
+    b = DescBuilder()
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(15, 15, 15))
+    clay = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.5, 0.6, 0.4))
+    cornell_room(b, white, red, light)
+    v = [[-4, 3, 0], [4, 3, 0], [0, 11, 0],          # 0-2: the tied pair's corners
+         [-6, 1, 2], [6, 1, 2], [6, 1.0000001, 2.5],   # 3-5: needle
+         [0, 2, -3], [0, 12, -3], [0, 7, 4],           # 6-8: edge-on to the camera (plane x = 0)
+         [2, 12, 1], [5, 14, 1], [3, 17, 1]]           # 9-11: a plain face
+    n = [[0, 0, -1], [0.4, 0.1, -1], [-0.3, 0.2, -1]]
+    faces = [[9, 10, 11], [0, 1, 2], [3, 4, 5], [0, 1, 2], [6, 7, 8], [0, 2, 1], [9, 11, 10], [3, 5, 4],
+             [6, 8, 7], [0, 1, 2]]
+    cn = [[0, 0, 0], [1, 1, 1], [0, 0, 0], [0, 0, 0], [0, 0, 0], [2, 2, 2], [0, 0, 0], [0, 0, 0], [0, 0, 0],
+          [2, 0, 1]]
+    b.mesh(clay, v, faces, normals=n, corner_normals=cn)
+    return b
+
+
+@pytest.mark.parametrize("small_mesh_tris", [16, 0])
+def test_face_ties_and_slivers_bit_exact(small_mesh_tris, gpu_renderer):
+    """Round 5's face tests (one plane compare over a quotient every lane
+    computes, the barycentric test as one NaN-safe compare, the (t, face)
+    order as one 64-bit key with the winning face held in a register) on
+    faces that tie in t, a needle and an edge-on face: as a small mesh
+    tested face by face and, with small_mesh_tris = 0, through the BVH walk;
+    every plane bit-exact with the oracle."""
+    gpu_renderer.set_options(small_mesh_tris=small_mesh_tris)
+    ptr = ties_scene().build()
+    out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    ref = oracle_render(ptr, CAM, 96, 72, 16)
+    assert_parity(out, ref, exact=True)
+
+
 def test_frosted_glass_within_tolerance(gpu_renderer):
     # frost > 0 rotates by cos/sin (vector3.h:315): ocml vs glibc may differ by an ulp
     b = zoo(frost=0.2)

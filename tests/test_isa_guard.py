@@ -2,7 +2,7 @@
 spills and VGPR budget, read from the gfx950 code object in libfsgpu.so.
 
 Several of the kernel's measured gains rest on how the compiler allocates
-registers (cold records read at their use, the integer-min
+registers (DESIGN_HISTORY.md §5: cold records read at their use, the integer-min
 slab clamp, the 6-wave launch bound); every 8-16 B/lane of extra spills has
 cost 1-2 %. A toolchain update or a source change that undoes them fails
 here before it reaches a GPU. Raising a limit is a deliberate edit, made
@@ -29,9 +29,9 @@ LIMITS = {
     # spills 12 -> 14 with the backward-pass material table's pointer and count
     # in the scene record (round 4; no bench config runs LEAN); 16 -> 24 with
     # the round-5 small-mesh face loop and no SLP vectorization (C2 and C3,
-    # which run the other kernels, +8.9 % and +3.0 %); 24 -> 48 with the
-    # round-5 node step (the parked-walk kernel's, above)
-    "render_kernel_lean<false, 6, false, false, false, false, false>": (48, 14, 80),
+    # which run the other kernels, +8.9 % and +3.0 %); 24 with the round-5
+    # node step and leaf-test plane compare
+    "render_kernel_lean<false, 6, false, false, false, false, false>": (24, 14, 80),
     # LEAN without walks (NOWALK: every mesh small, no walk stack, 8 waves per
     # SIMD): C1 and C2. 44 -> 40 B/lane without the backward pass (C2 +8.5 %);
     # 40 -> 48 with the round-5 face loop (one branch per face) and no SLP
