@@ -1,0 +1,97 @@
+"""The kernels rewrite a few of the reference's float expressions into cheaper
+forms that must round identically (DESIGN.md §2 "How bit-exactness is kept").
+These CPU checks restate each rewrite in numpy float32 next to the reference
+form and compare bit patterns over special values (signed zeros, subnormals,
+infinities, NaN) and random operands. The GPU parity tests check the kernels
+themselves; these pin the algebra the kernels rely on."""
+import itertools
+
+import numpy as np
+
+f32 = np.float32
+SPECIAL = [0.0, -0.0, 1.0, -1.0, 0.5, 1.5, -1.5, 1e-45, -1e-45, 1.2e-38, -1.2e-38, 3e38, -3e38,
+           np.inf, -np.inf, 2.0, -2.0, 1.0 - 2.0 ** -24, 1.0 + 2.0 ** -23]
+
+
+def bits(x):
+    return np.asarray(x, dtype=np.float32).view(np.uint32)
+
+
+def same(a, b):
+    """bitwise equal, any NaN equal to any NaN"""
+    a = np.asarray(a, dtype=np.float32)
+    b = np.asarray(b, dtype=np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return np.all(both_nan | (bits(a) == bits(b)))
+
+
+def operands(n=200000, seed=7):
+    rng = np.random.default_rng(seed)
+    sp = np.array(SPECIAL, dtype=np.float32)
+    a = np.array([x for x, _ in itertools.product(sp, sp)], dtype=np.float32)
+    b = np.array([y for _, y in itertools.product(sp, sp)], dtype=np.float32)
+    # random magnitudes over many binades, both signs, plus exact cancellations
+    ra = (rng.standard_normal(n) * 10.0 ** rng.integers(-6, 6, n)).astype(np.float32)
+    rb = (rng.standard_normal(n) * 10.0 ** rng.integers(-6, 6, n)).astype(np.float32)
+    rb[: n // 10] = -ra[: n // 10]
+    return np.concatenate([a, ra]), np.concatenate([b, rb])
+
+
+def test_planar_dot_is_sum_plus_zero():
+    """bary_pre (fs_device.hip): the reference's 3-term dot over planar-mapped
+    vectors, ((0 + A) + B), ((A + 0) + B) or ((A + B) + 0) by axis
+    (intersect.cpp:146-177), equals (A + B) + 0 bit for bit."""
+    A, B = operands()
+    z = f32(0.0)
+    with np.errstate(all="ignore"):
+        new = (A + B) + z
+        for ref in ((z + A) + B, (A + z) + B, (A + B) + z):
+            assert same(ref, new)
+
+
+def test_barycentric_sum_test_as_difference():
+    """(uu + vv <= 1) is 1 - (uu + vv) >= 0 exactly, and min(uu, vv, w) + (w - w) >= 0
+    is the reference's three-way test, NaN failing both (small_face_hit, leaf_tri)."""
+    U, V = operands(seed=11)
+    one = f32(1.0)
+    with np.errstate(all="ignore"):
+        s = U + V
+        w = one - s
+        ref = (U >= 0) & (V >= 0) & (s <= one)
+        m = np.fmin(np.fmin(U, V), w) + (w - w)  # fmin: NaN-ignoring, as v_min_f32
+        new = m >= 0
+    assert np.array_equal(ref, new)
+
+
+def test_plane_range_test_as_one_compare():
+    """ray_plane (intersect.cpp:728-744): !cmp_eps(ts, 0) && 0 <= ns/ts <= 1 is
+    med3(q, 0, 1) == q over q = ns/ts forced to -1 where |ts| < eps; med3 here is
+    the NaN-ignoring clamp v_med3_f32 computes (a NaN q fails the compare)."""
+    eps = f32(1e-6)  # kEpsilon's role; the identity holds for any eps > 0
+    NS, TS = operands(seed=3)
+    with np.errstate(all="ignore"):
+        q = NS / TS
+        ref = ~(np.abs(TS) < eps) & (f32(0) <= q) & (q <= f32(1))
+        qf = np.where(np.abs(TS) < eps, f32(-1.0), q)
+        med = np.fmax(np.fmin(qf, f32(1.0)), f32(0.0))
+        new = med == qf
+    assert np.array_equal(ref, new)
+
+
+def test_closest_hit_key_orders_as_reference():
+    """The (t, face) order as one 64-bit key (small_face_hit, leaf_tri): for hits
+    with t >= 0 (or -0), key < best is `t < h.t || (t == h.t && face < bface)`,
+    with t + 0 turning -0 into +0 so the bits order as unsigned integers."""
+    rng = np.random.default_rng(5)
+    n = 100000
+    pool = np.array([0.0, -0.0, 1e-45, 0.25, 0.5, 1.0, 2.0], dtype=np.float32)
+    t = np.where(rng.random(n) < 0.5, rng.choice(pool, n), rng.random(n).astype(np.float32))
+    ht = np.where(rng.random(n) < 0.5, rng.choice(pool, n), rng.random(n).astype(np.float32))
+    t = t.astype(np.float32)
+    ht = ht.astype(np.float32)
+    face = rng.integers(0, 8, n).astype(np.uint64)
+    bface = rng.integers(0, 8, n).astype(np.uint64)
+    ref = (t < ht) | ((t == ht) & (face < bface))
+    key = (bits(t + f32(0)).astype(np.uint64) << np.uint64(32)) | face
+    best = (bits(ht + f32(0)).astype(np.uint64) << np.uint64(32)) | bface
+    assert np.array_equal(ref, key < best)

@@ -28,7 +28,7 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 def build(out="/tmp/fs_isa_lines.o", extra=()):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-g", "-std=c++17", "-ffp-contract=off",
-           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"), "--cuda-device-only", "-c",
+           "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"), "--cuda-device-only", "-c",
            os.path.join(PKG, "csrc", "fs_device.hip"), "-o", out, *extra]
     subprocess.run(cmd, check=True)
     co = out + ".co"
@@ -77,11 +77,17 @@ def attribute(co, prefix):
 
 def main():
     prefix = sys.argv[1] if len(sys.argv) > 1 else "Lb0ELi6ELb0ELb1ELb0ELb0ELb0ELb0E"
-    ranges = sys.argv[2:]
+    ranges = [a for a in sys.argv[2:] if a != "--scratch"]
     co = build()
     name, rows = attribute(co, prefix)
     total = collections.Counter(kind(m) for _, m in rows)
     print(f"{name[:90]}...: {len(rows)} instructions {dict(total)}")
+    if "--scratch" in sys.argv:
+        # where the spills are: scratch loads and stores by source line
+        sc = collections.Counter((f, ln, m) for (f, ln), m in rows if m.startswith("scratch_"))
+        for (f, ln, m), n in sorted(sc.items(), key=lambda kv: (kv[0][0], kv[0][1])):
+            print(f"{f}:{ln}  {m} x{n}")
+        return
     if ranges:
         for rg in ranges:
             fname, span = rg.split(":")
