@@ -335,16 +335,16 @@ __device__ __forceinline__ uint32_t tri_face(const DevTri* __restrict__ T, uint3
 // intersect.cpp:146-177 with the triangle-only terms precomputed. The
 // reference's 3-term dot products over the planar-mapped vectors carry an
 // exact +0 term for the zeroed axis: ((0 + A) + B) for axis x, ((A + 0) + B)
-// for y and ((A + B) + 0) for z, restated here with the same rounding.
+// for y and ((A + B) + 0) for z. All three equal (A + B) + 0 bit for bit: each
+// is A + B except that none gives -0 (-0 arises only from -0 + -0, and an
+// exact +0 term turns it into +0 in any position; NaN stays NaN), so the
+// axis selects no operand order.
 __device__ __forceinline__ void bary_pre(const TriData& T, f3 pt, float& u, float& v) {
   const bool az = T.axis == 2;
   const float pa = T.axis == 0 ? pt.y : pt.x, pb = az ? pt.y : pt.z;
   const float va = pa - T.p1a, vb = pb - T.p1b;
-  float A = T.v0a * va, B = T.v0b * vb;
-  const float d02 = (A + (az ? B : 0.0f)) + (az ? 0.0f : B);
-  A = T.v1a * va;
-  B = T.v1b * vb;
-  const float d12 = (A + (az ? B : 0.0f)) + (az ? 0.0f : B);
+  const float d02 = (T.v0a * va + T.v0b * vb) + 0.0f;
+  const float d12 = (T.v1a * va + T.v1b * vb) + 0.0f;
   u = (T.d11 * d02 - T.d01 * d12) * T.inv;
   v = (T.d00 * d12 - T.d01 * d02) * T.inv;
 }
@@ -803,9 +803,13 @@ __device__ __forceinline__ void test_leaf(const DevScene& S, uint32_t w, int32_t
 // unsigned integers once -0 becomes +0), with the best face 0 unless this
 // call wrote h (h.obj == oi only then: objects are traced once per
 // segment), so "lower face first among equal t" needs no object compare and
-// no load of the best face's record.
-__device__ __forceinline__ void small_face_hit(const TriData& T, uint32_t ti, int32_t oi, float tt, f3 pp, uint32_t point,
-                                               MinHit& h, uint32_t& bface) {
+// no load of the best face's record. ONCE (the kernel without walks): h.obj
+// and h.point are set once per mesh from a lane mask of the faces that won
+// (C2 +1.4 %; C4 -0.6 % in the walking kernels, whose SGPR budget the extra
+// mask strains: round 5, profiles/r05/ab_spills.log).
+template <bool ONCE>
+__device__ __forceinline__ void small_face_hit(const TriData& T, uint32_t ti, int32_t oi, float tt, f3 pp,
+                                               uint32_t point, MinHit& h, uint32_t& bface, bool& wrote) {
   float uu, vv;
   bary_pre(T, pp, uu, vv);
   const float w = 1.0f - (uu + vv);
@@ -814,12 +818,16 @@ __device__ __forceinline__ void small_face_hit(const TriData& T, uint32_t ti, in
   const uint64_t best = ((uint64_t)__float_as_uint(h.t + 0.0f) << 32) | bface;
   const bool better = key < best;
   h.t = better ? tt : h.t;
-  h.obj = better ? oi : h.obj;
   h.prim = better ? ti : h.prim;
   h.u = better ? uu : h.u;
   h.v = better ? vv : h.v;
-  h.point = better ? point : h.point;
   bface = better ? T.face : bface;
+  if (ONCE) {
+    wrote = wrote || better;
+  } else {
+    h.obj = better ? oi : h.obj;
+    h.point = better ? point : h.point;
+  }
 }
 // The faces of a small mesh for the lanes of non-zero-length rays.
 // ray_plane (intersect.cpp:728-744) is a hit when !cmp_eps(ts, 0) and
@@ -829,10 +837,11 @@ __device__ __forceinline__ void small_face_hit(const TriData& T, uint32_t ti, in
 // arithmetic on the scalar unit. The quotient is taken on every lane (the
 // empty asm keeps the compiler from putting the division behind a branch of
 // its own).
-template <bool COUNT>
+template <bool COUNT, bool ONCE>
 __device__ __forceinline__ void small_mesh_rays(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
                                                 const Ray& r, MinHit& h, Tally<COUNT>& tally) {
   bool on_plane = false;  // the plane test of the last distinct plane
+  bool wrote = false;
   float tt = 0.0f;
   f3 pp = mk3(0, 0, 0);
   uint32_t bface = 0;
@@ -850,29 +859,38 @@ __device__ __forceinline__ void small_mesh_rays(const DevScene& S, uint32_t firs
       tt = q;
       pp = r.start + r.dir * q;
     }
-    if (on_plane) small_face_hit(T, ti, oi, tt, pp, 0u, h, bface);
+    if (on_plane) small_face_hit<ONCE>(T, ti, oi, tt, pp, 0u, h, bface, wrote);
+  }
+  if (ONCE) {
+    h.obj = wrote ? oi : h.obj;
+    h.point = wrote ? 0u : h.point;
   }
 }
 // The same for the lanes of zero-length rays (total internal reflection,
 // rare): point_in_tri (intersect.cpp:320-346), t = 0 at the segment start.
-template <bool COUNT>
+template <bool COUNT, bool ONCE>
 __device__ __forceinline__ void small_mesh_points(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
                                                   const Ray& r, MinHit& h) {
   uint32_t bface = 0;
+  bool wrote = false;
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t ti = first + i;
     TriData T = load_tri_uniform(S.tris, ti);
     const float d4 = T.pl.x * r.start.x + T.pl.y * r.start.y + T.pl.z * r.start.z + T.pl.w * 1.0f;
-    if (cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) small_face_hit(T, ti, oi, 0.0f, r.start, 1u, h, bface);
+    if (cmp_eps(d4 + T.pl.w, 0.0f, kEpsilon)) small_face_hit<ONCE>(T, ti, oi, 0.0f, r.start, 1u, h, bface, wrote);
+  }
+  if (ONCE) {
+    h.obj = wrote ? oi : h.obj;
+    h.point = wrote ? 1u : h.point;
   }
 }
 // A lane runs the faces of its kind of ray; zero-length rays are tested in a
 // second loop that runs only when the wave holds one.
-template <bool COUNT>
+template <bool COUNT, bool ONCE = false>
 __device__ __forceinline__ void small_mesh_trace(const DevScene& S, uint32_t first, uint32_t n, int32_t oi,
                                                  const Ray& r, bool zl, MinHit& h, Tally<COUNT>& tally) {
-  if (!zl) small_mesh_rays<COUNT>(S, first, n, oi, r, h, tally);
-  if (__ballot(zl) && zl) small_mesh_points<COUNT>(S, first, n, oi, r, h);
+  if (!zl) small_mesh_rays<COUNT, ONCE>(S, first, n, oi, r, h, tally);
+  if (__ballot(zl) && zl) small_mesh_points<COUNT, ONCE>(S, first, n, oi, r, h);
 }
 
 // SUSP: when at most `thr` lanes are still walking while other live lanes of
@@ -979,7 +997,10 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
     if (SUSP && susp) break;
     // One triangle per lane per trip, running on through the leaves the walk
     // stopped on (the popped far children may be leaves too), so a lane with
-    // 1+2 triangles costs the wave 3 trips, not max-per-leaf 2+2.
+    // 1+2 triangles costs the wave 3 trips, not max-per-leaf 2+2. (Selects for
+    // this step and a branch-free triangle test with the (t, face) key, as the
+    // node step and the small-mesh faces, measured C4 -3 %, C3 -5 %: round 5,
+    // profiles/r05/ab_spills_leaf.log.)
     while (leaf) {
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.leaf_trips);
@@ -1011,19 +1032,17 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
 }
 
 // Conservative segment-vs-box cull for analytic objects (not a reference
-// test): the slab interval uses v_rcp and the same t margins as the BVH
-// traversal, against a box padded on the host (fs_scene.cpp). A segment that
-// can produce a hit with t < best always passes.
+// test): the slab interval over the segment's slopes (seg_slopes, the ones
+// the mesh-root culls and walks use; dir and stop - start differ by rounding
+// only) with the BVH traversal's t margins, against a box padded on the host
+// (fs_scene.cpp). A segment that can produce a hit with t < best always
+// passes. (Slopes of its own from r.dir cost three v_rcp per segment, which
+// the compiler hoisted out of the object loop and spilled.)
 template <class FloatPtr>
-__device__ __forceinline__ bool seg_box_cull(const Ray& r, float best, FloatPtr b) {
-  const float tiny = 1e-20f;
-  float dx = fabsf(r.dir.x) < tiny ? copysignf(tiny, r.dir.x) : r.dir.x;
-  float dy = fabsf(r.dir.y) < tiny ? copysignf(tiny, r.dir.y) : r.dir.y;
-  float dz = fabsf(r.dir.z) < tiny ? copysignf(tiny, r.dir.z) : r.dir.z;
-  float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
-  float a0 = (b[0] - r.start.x) * ix, a1 = (b[3] - r.start.x) * ix;
-  float c0 = (b[1] - r.start.y) * iy, c1 = (b[4] - r.start.y) * iy;
-  float e0 = (b[2] - r.start.z) * iz, e1 = (b[5] - r.start.z) * iz;
+__device__ __forceinline__ bool seg_box_cull(const Slopes& sl, float best, FloatPtr b) {
+  float a0 = fmaf(b[0], sl.ix, sl.ox), a1 = fmaf(b[3], sl.ix, sl.ox);
+  float c0 = fmaf(b[1], sl.iy, sl.oy), c1 = fmaf(b[4], sl.iy, sl.oy);
+  float e0 = fmaf(b[2], sl.iz, sl.oz), e1 = fmaf(b[5], sl.iz, sl.oz);
   float tn = fmaxf(fmaxf(fminf(a0, a1), fminf(c0, c1)), fmaxf(fminf(e0, e1), -1e-6f));
   float tf = fminf(fminf(fmaxf(a0, a1), fmaxf(c0, c1)), fminf(fmaxf(e0, e1), fminf(best, 1.0f) * 1.000002f + 1e-7f));
   return tn <= tf;
@@ -1097,7 +1116,7 @@ __device__ __forceinline__ bool object_trace(const DevScene& S, uint32_t oi, con
       hit = !(fabsf(bd) > d[7] || fabsf(td) > d[8]) && t < h.t;
     }
   } else if (kind == FS_OBJ_CUBOID) {
-    if (seg_box_cull(r, h.t, d + 24)) {
+    if (seg_box_cull(*slp, h.t, d + 24)) {
       for (uint32_t i = 0; i < 6; i++) {
         float ti;
         if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, ti, p) && ti < h.t) {
@@ -1282,7 +1301,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
       uint64_t t1 = FS_TICK();
       if (H.i3) {  // a small mesh: its faces, no walk (never parks)
         if (visit)
-          small_mesh_trace<COUNT>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
+          small_mesh_trace<COUNT, NOWALK>(S, __float_as_uint(hd[6]), (uint32_t)H.i3, (int32_t)oi, r, zl, h, tally);
 #ifdef FS_PHASE_PROF
         {  // the faces are their own phase: neither the cull's nor the walk's
           const uint64_t ts = FS_TICK() - t1;
@@ -1364,7 +1383,7 @@ __device__ __forceinline__ void scene_trace_min(const DevScene& S, const Ray& r,
         }
       }
     } else if (kind == FS_OBJ_CUBOID) {
-      if (!seg_box_cull(r, h.t, d + 24)) continue;
+      if (!seg_box_cull(sl, h.t, d + 24)) continue;
       for (uint32_t i = 0; i < 6; i++) {
         if (ray_plane(mk4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]), r, t, p) && t < h.t) {
           bool ok = true;
@@ -1814,7 +1833,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
           at_byte(Fz.normal, pix * 12u)[0] = nd.x;
           at_byte(Fz.normal, pix * 12u)[1] = nd.y;
           at_byte(Fz.normal, pix * 12u)[2] = nd.z;
-          *at_byte(Fz.depth, pix * 4u) = C.z_far;
+          *at_byte(Fz.depth, pix * 4u) = at_use(C, cur.sample0 >> 31).z_far;
           *at_byte(Fz.material, pix * 8u) = Sz.sky_id;
         }
         done = true;

@@ -21,22 +21,20 @@ LIMITS = {
     # backward pass left the kernel for fold_paths (round 4: C4 +4.5 %,
     # profiles/r04/ab_records.log); 40 -> 28 without SLP vectorization (round 5:
     # C4 +7.4 %, profiles/r05/ab_noslp.log); 28 -> 48 with the node step as
-    # selects and wave-uniform node-loop exits plus the table-driven
-    # Material::Reflection (C3 +2.6 %, C4 +2.8 %, profiles/r05/ab_nodesel.log;
-    # the spills sit outside the node and face loops)
-    "render_kernel_lean<false, 6, false, true, false, false, false>": (48, 14, 80),
-    # LEAN schedule: scenes with BVH walks and no large mesh. 16 B/lane; SGPR
-    # spills 12 -> 14 with the backward-pass material table's pointer and count
-    # in the scene record (round 4; no bench config runs LEAN); 16 -> 24 with
-    # the round-5 small-mesh face loop and no SLP vectorization (C2 and C3,
-    # which run the other kernels, +8.9 % and +3.0 %); 24 with the round-5
-    # node step and leaf-test plane compare
-    "render_kernel_lean<false, 6, false, false, false, false, false>": (24, 14, 80),
+    # selects (C4 +2.8 %, profiles/r05/ab_nodesel.log); 48 -> 20 once the
+    # cuboid cull took the segment's slopes instead of three v_rcp of its own
+    # that the compiler hoisted out of the object loop and spilled (C4 +4 %,
+    # C2 +5 %, write-backs 176 -> 95 B per sample, profiles/r05/ab_spills.log)
+    "render_kernel_lean<false, 6, false, true, false, false, false>": (24, 14, 80),
+    # LEAN schedule: scenes with BVH walks and no large mesh (no bench config
+    # runs it). 24 -> 12 B/lane with the cuboid cull on the segment's slopes
+    "render_kernel_lean<false, 6, false, false, false, false, false>": (16, 14, 80),
     # LEAN without walks (NOWALK: every mesh small, no walk stack, 8 waves per
     # SIMD): C1 and C2. 44 -> 40 B/lane without the backward pass (C2 +8.5 %);
-    # 40 -> 48 with the round-5 face loop (one branch per face) and no SLP
-    # vectorization: SALU per face 55 -> 17, C2 +8.9 % (profiles/r05/ab_noslp.log)
-    "render_kernel_lean<false, 8, false, false, false, false, true>": (48, 27, 64),
+    # 40 -> 48 with the round-5 face loop and no SLP vectorization (C2 +8.9 %,
+    # profiles/r05/ab_noslp.log); 48 -> 24 with the cuboid cull on the
+    # segment's slopes (profiles/r05/ab_spills.log)
+    "render_kernel_lean<false, 8, false, false, false, false, true>": (24, 16, 64),
 }
 
 

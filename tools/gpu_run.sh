@@ -85,11 +85,11 @@ for step in "$@"; do
       for i in $(seq 1 ${a4:-2}); do
         for L in $a1; do
           echo "== $L" >> $log
-          FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/$L timeout -k 10 300 \
+          PERF_AB_HASH=1 FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/$L timeout -k 10 300 \
             python tools/perf_ab.py default "$a2" ${a3:-256} 1 >> $log 2>&1 || fail "$step" $? $log
         done
       done
-      grep -E "^==|variant" $log ;;
+      grep -E "^==|variant|md5" $log ;;
     phase)
       FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/libfsgpu_prof.so timeout -k 10 600 \
         python tools/phase_prof.py "$a1" ${a2:-64} > $OUT/phase.log 2>&1 || fail "$step" $? $OUT/phase.log
