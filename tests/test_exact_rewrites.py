@@ -51,7 +51,7 @@ def test_planar_dot_is_sum_plus_zero():
 
 def test_barycentric_sum_test_as_difference():
     """(uu + vv <= 1) is 1 - (uu + vv) >= 0 exactly, and min(uu, vv, w) + (w - w) >= 0
-    is the reference's three-way test, NaN failing both (small_face_hit, leaf_tri)."""
+    is the reference's three-way test, NaN failing both (small_face_hit)."""
     U, V = operands(seed=11)
     one = f32(1.0)
     with np.errstate(all="ignore"):
@@ -79,7 +79,7 @@ def test_plane_range_test_as_one_compare():
 
 
 def test_closest_hit_key_orders_as_reference():
-    """The (t, face) order as one 64-bit key (small_face_hit, leaf_tri): for hits
+    """The (t, face) order as one 64-bit key (small_face_hit): for hits
     with t >= 0 (or -0), key < best is `t < h.t || (t == h.t && face < bface)`,
     with t + 0 turning -0 into +0 so the bits order as unsigned integers."""
     rng = np.random.default_rng(5)
@@ -95,3 +95,34 @@ def test_closest_hit_key_orders_as_reference():
     key = (bits(t + f32(0)).astype(np.uint64) << np.uint64(32)) | face
     best = (bits(ht + f32(0)).astype(np.uint64) << np.uint64(32)) | bface
     assert np.array_equal(ref, key < best)
+
+
+def _quake_len(d):
+    """base::sqrtf (scalar.h:233-245) in float32: 1 / inv_sqrt(d), one Newton step."""
+    d = np.asarray(d, dtype=np.float32)
+    half = f32(0.5) * d
+    i = (np.int32(0x5F3759DF) - (d.view(np.int32) >> 1)).astype(np.int32)
+    f = i.view(np.float32)
+    with np.errstate(all="ignore"):
+        f = f * (f32(1.5) - (half * f) * f)
+        return f32(1.0) / f
+
+
+def test_zero_length_shortcut():
+    """zero_len (fs_device.hip): a dot(dir, dir) in [1e-9, 1e30] never gives a
+    length within kEpsilon = 1e-5 of zero, so only the rest takes the division;
+    an infinite dot gives length -0 (zero-length), which the shortcut leaves to
+    the division."""
+    eps = f32(1e-5)
+    lo, hi = np.float32(1e-9), np.float32(1e30)
+    rng = np.random.default_rng(13)
+    d = np.concatenate([
+        np.geomspace(1e-9, 1e30, 400001).astype(np.float32),
+        np.nextafter(lo, np.float32(np.inf), dtype=np.float32)[None],
+        np.array([lo, hi], dtype=np.float32),
+        (10.0 ** rng.uniform(-9, 30, 200000)).astype(np.float32),
+    ])
+    d = d[(d >= lo) & (d <= hi)]
+    ln = _quake_len(d)
+    assert np.all(~((ln > -eps) & (ln < eps)))
+    assert _quake_len(np.float32(np.inf)) == 0.0  # -0: zero-length in the reference
