@@ -1,0 +1,103 @@
+"""Seeded random scenes against the oracle, every plane bit-exact.
+
+The fixed scenes (C1-C4, the material zoo, the tie scene) pin the kernels on
+hand-picked geometry; these draw the geometry: spheres, planes, discs, both
+quad kinds and rotated cuboids at random places and sizes, small meshes of
+random faces (tested face by face), and a cloud of random triangles large
+enough for a BVH walk (with parking forced on one schedule), in the Cornell
+room, with every material whose path needs no device transcendental (no
+frost, no thin lens). Objects overlap, intersect and nest at random, so
+segments start inside boxes, graze faces and tie more often than in the bench
+scenes."""
+import numpy as np
+import pytest
+
+import fsamd
+from descbuild import DescBuilder, cornell_room
+from test_gpu_parity import assert_parity, gpu_render, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+
+def random_scene(seed, cloud_tris=3000):
+    rng = np.random.default_rng(seed)
+    b = DescBuilder()
+    white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
+    red = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.65, 0.05, 0.05))
+    light = b.material(fsamd.MAT_LIGHT, emissive=(12, 12, 12))
+    u = lambda lo, hi: float(rng.uniform(lo, hi))  # noqa: E731
+    col = lambda: tuple(float(x) for x in rng.uniform(0.2, 0.95, 3))  # noqa: E731
+    mats = [
+        b.material(fsamd.MAT_DIFFUSE, diffuse=col()),
+        b.material(fsamd.MAT_METAL, diffuse=col(), roughness=u(0.0, 1.0)),
+        b.material(fsamd.MAT_MIRROR, diffuse=col()),
+        b.material(fsamd.MAT_GLASS, diffuse=col(), index=u(0.5, 1.6), reflectivity=u(0.0, 0.5)),
+        b.material(fsamd.MAT_LIQUID, diffuse=col(), index=u(1.1, 1.6), reflectivity=u(0.0, 0.5)),
+        b.material(fsamd.MAT_CERAMIC, diffuse=col(), shininess=u(0.0, 1.0)),
+        b.material(fsamd.MAT_GLOW, diffuse=col(), glow=col(), shininess=u(0.0, 1.0)),
+        b.material(fsamd.MAT_FOG, diffuse=col(), density=u(0.001, 0.05)),
+        b.material(fsamd.MAT_LIGHT, emissive=tuple(3 * x for x in col())),
+    ]
+    pick = lambda: mats[int(rng.integers(len(mats)))]  # noqa: E731
+    cornell_room(b, white, red, light)
+    p = lambda: [u(-8, 8), u(1, 18), u(-8, 8)]  # noqa: E731
+    n = lambda: list(rng.normal(size=3))  # noqa: E731
+    for _ in range(int(rng.integers(2, 5))):
+        b.obj(fsamd.OBJ_SPHERE, pick(), p() + [u(0.5, 3)])
+    if rng.random() < 0.5:
+        nv = np.array(n())
+        nv /= np.linalg.norm(nv)
+        b.obj(fsamd.OBJ_PLANE, pick(), list(nv) + [u(-9, 9)])
+    for _ in range(int(rng.integers(1, 3))):
+        b.obj(fsamd.OBJ_DISC, pick(), p() + n() + [u(0.5, 4)])
+    for _ in range(int(rng.integers(1, 3))):
+        b.obj(fsamd.OBJ_QUAD_ONWH, pick(), p() + n() + [u(1, 6), u(1, 6)])
+    for _ in range(int(rng.integers(1, 3))):
+        b.obj(fsamd.OBJ_QUAD_PUV, pick(), p() + [u(-4, 4) for _ in range(6)])
+    for _ in range(int(rng.integers(1, 3))):
+        b.obj(fsamd.OBJ_CUBOID, pick(), p() + [u(0.5, 4), u(0.5, 4), u(0.5, 4)] + n() + [u(-3, 3)],
+              rotate=int(rng.integers(0, 2)))
+    for _ in range(int(rng.integers(2, 4))):  # small meshes: random faces, some sharing an edge
+        nf = int(rng.integers(2, 15))
+        c = np.array(p())
+        v = c + rng.normal(scale=u(0.5, 3), size=(nf + 2, 3))
+        faces = [[0, 1, i + 2] if rng.random() < 0.3 else list(rng.choice(nf + 2, 3, replace=False))
+                 for i in range(nf)]
+        b.mesh(pick(), v.tolist(), faces)
+    # a triangle cloud for the BVH walk: small faces around random centres
+    c = np.array(p())
+    centres = c + rng.normal(scale=3.0, size=(cloud_tris, 1, 3))
+    tv = (centres + rng.normal(scale=0.35, size=(cloud_tris, 3, 3))).reshape(-1, 3)
+    b.mesh(pick(), tv.tolist(), np.arange(3 * cloud_tris).reshape(-1, 3).tolist(),
+           rotation=(0, 1, 0, u(-1, 1)), scale=(u(0.7, 1.3),) * 3)
+    return b
+
+
+CAMS = [fsamd.camera((0, 10, -34), (0, 10, 0), fov_y=40, aperture=0.0),
+        fsamd.camera((-8, 15, -9), (4, 6, 5), fov_y=70, aperture=0.0)]
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_scene_bit_exact(seed, gpu_renderer):
+    """Sixteen seeded scenes, two camera placements (one inside the clutter)."""
+    b = random_scene(seed)  # keeps the arrays the description points at alive
+    ptr = b.build()
+    cam = CAMS[seed % 2]
+    out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    ref = oracle_render(ptr, cam, 80, 60, 8)
+    assert_parity(out, ref, exact=True)
+
+
+@pytest.mark.parametrize("schedule,seed", [("parked", 100), ("parked", 101), ("parked", 102), ("parked", 103),
+                                           ("lean", 200), ("lean", 201)])
+def test_random_scene_schedules_bit_exact(schedule, seed, gpu_renderer):
+    """The parked-walk kernel (C3 and C4's) with parking forced for the
+    triangle cloud (park_min_tris = 1), and the lean kernel, on random
+    clutter."""
+    gpu_renderer.set_options(schedule=schedule, park_min_tris=1)
+    b = random_scene(seed)  # keeps the arrays the description points at alive
+    ptr = b.build()
+    cam = CAMS[seed % 2]
+    out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    ref = oracle_render(ptr, cam, 80, 60, 8)
+    assert_parity(out, ref, exact=True)
