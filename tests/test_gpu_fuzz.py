@@ -19,7 +19,7 @@ from test_gpu_parity import assert_parity, gpu_render, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-def random_scene(seed, cloud_tris=3000):
+def random_scene(seed, cloud_tris=3000, crowd=0):
     rng = np.random.default_rng(seed)
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
@@ -64,6 +64,17 @@ def random_scene(seed, cloud_tris=3000):
         faces = [[0, 1, i + 2] if rng.random() < 0.3 else list(rng.choice(nf + 2, 3, replace=False))
                  for i in range(nf)]
         b.mesh(pick(), v.tolist(), faces)
+    for j in range(crowd):  # many small analytic objects (the object-octree threshold is 182)
+        k = int(rng.integers(4))
+        if k == 0:
+            b.obj(fsamd.OBJ_SPHERE, pick(), p() + [u(0.2, 0.9)])
+        elif k == 1:
+            b.obj(fsamd.OBJ_CUBOID, pick(), p() + [u(0.3, 1.2), u(0.3, 1.2), u(0.3, 1.2)] + n() + [u(-3, 3)],
+                  rotate=1)
+        elif k == 2:
+            b.obj(fsamd.OBJ_DISC, pick(), p() + n() + [u(0.3, 1.0)])
+        else:
+            b.obj(fsamd.OBJ_QUAD_PUV, pick(), p() + [u(-1, 1) for _ in range(6)])
     # a triangle cloud for the BVH walk: small faces around random centres
     c = np.array(p())
     centres = c + rng.normal(scale=3.0, size=(cloud_tris, 1, 3))
@@ -99,5 +110,20 @@ def test_random_scene_schedules_bit_exact(schedule, seed, gpu_renderer):
     ptr = b.build()
     cam = CAMS[seed % 2]
     out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    ref = oracle_render(ptr, cam, 80, 60, 8)
+    assert_parity(out, ref, exact=True)
+
+
+@pytest.mark.parametrize("optimized,seed", [(True, 300), (True, 301), (False, 302)])
+def test_random_crowd_bit_exact(optimized, seed, gpu_renderer):
+    """About 200 random objects: optimized, traced through the reference's
+    object octree (scene.cpp:11-133, the SOCT kernel), else down the object
+    list."""
+    b = random_scene(seed, cloud_tris=500, crowd=190)
+    ptr = b.build(optimized=optimized)
+    cam = CAMS[seed % 2]
+    out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    k = gpu_renderer.last_kernel()
+    assert (k[:-1].split(", ")[5] == "true") == optimized, k
     ref = oracle_render(ptr, cam, 80, 60, 8)
     assert_parity(out, ref, exact=True)
