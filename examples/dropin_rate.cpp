@@ -1,0 +1,59 @@
+// dropin_rate.cpp — samples/s of the drop-in API as an application drives it
+// (measurement aid for DESIGN.md §6): the reference's window loop calls
+// TraceScene once per displayed frame and reads the display bytes back
+// (main.cpp:157-162), so every frame of 1 spp pays a launch, a fold and a
+// PCIe read of W x H x 3 bytes; TraceSceneBatch submits many samples at once.
+// Scene load and BVH build are excluded (one warm-up frame first).
+//
+//   dropin_rate <file.scene> <width> <height> <frames>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
+#include "fs_host.h"
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    std::fprintf(stderr, "usage: %s scene width height frames\n", argv[0]);
+    return 2;
+  }
+  base::Scene scene;
+  if (!scene.LoadScene(argv[1])) return 1;
+  base::InitializeMaterials();
+  base::Camera camera;
+  if (scene.GetCameraCount()) camera = *scene.GetCamera(0);
+  const unsigned W = std::atoi(argv[2]), H = std::atoi(argv[3]), frames = std::atoi(argv[4]);
+  base::DisplayFrame frame(W, H);
+  base::TraceScene(camera, &scene, &frame);  // upload + BVH build, not timed
+  frame.GetDisplayBuffer();
+  if (base::LastTraceStatus() != 0) {
+    std::fprintf(stderr, "TraceScene failed: %s\n", base::LastTraceError());
+    return 1;
+  }
+  // the window loop: one TraceScene (1 spp) and one display read per frame
+  double t0 = now_s();
+  for (unsigned i = 0; i < frames; i++) {
+    base::TraceScene(camera, &scene, &frame);
+    frame.GetDisplayBuffer();
+  }
+  const double loop_s = now_s() - t0;
+  // the same samples in one submission, one display read
+  frame.Reset();
+  t0 = now_s();
+  base::TraceSceneBatch(camera, &scene, &frame, frames);
+  frame.GetDisplayBuffer();
+  const double batch_s = now_s() - t0;
+  if (base::LastTraceStatus() != 0) {
+    std::fprintf(stderr, "trace failed: %s\n", base::LastTraceError());
+    return 1;
+  }
+  const double samples = (double)W * H * frames;
+  std::printf("{\"width\": %u, \"height\": %u, \"frames\": %u, \"loop_msamples_per_s\": %.2f, "
+              "\"loop_ms_per_frame\": %.3f, \"batch_msamples_per_s\": %.2f}\n",
+              W, H, frames, samples / loop_s / 1e6, loop_s * 1e3 / frames, samples / batch_s / 1e6);
+  return 0;
+}
