@@ -19,7 +19,7 @@ from test_gpu_parity import assert_parity, gpu_render, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-def random_scene(seed, cloud_tris=3000, crowd=0):
+def random_scene(seed, cloud_tris=3000, crowd=0, textured=False):
     rng = np.random.default_rng(seed)
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
@@ -39,6 +39,12 @@ def random_scene(seed, cloud_tris=3000, crowd=0):
         b.material(fsamd.MAT_LIGHT, emissive=tuple(3 * x for x in col())),
     ]
     pick = lambda: mats[int(rng.integers(len(mats)))]  # noqa: E731
+    flat = pick  # materials of objects whose texture lookup is bit-exact (planar maps, mesh texcoords)
+    if textured:  # diffuse maps of random sizes and scales; spheres (atan2f maps) never take them
+        tex = [b.texture(rng.random((int(rng.integers(2, 40)), int(rng.integers(2, 40)), 3)) * u(0.3, 2.0))
+               for _ in range(2)]
+        tmats = [b.material(fsamd.MAT_DIFFUSE, diffuse=col(), texture=t, texture_scale=u(0.05, 3.0)) for t in tex]
+        flat = lambda: tmats[int(rng.integers(2))] if rng.random() < 0.6 else pick()  # noqa: E731
     cornell_room(b, white, red, light)
     p = lambda: [u(-8, 8), u(1, 18), u(-8, 8)]  # noqa: E731
     n = lambda: list(rng.normal(size=3))  # noqa: E731
@@ -47,15 +53,15 @@ def random_scene(seed, cloud_tris=3000, crowd=0):
     if rng.random() < 0.5:
         nv = np.array(n())
         nv /= np.linalg.norm(nv)
-        b.obj(fsamd.OBJ_PLANE, pick(), list(nv) + [u(-9, 9)])
+        b.obj(fsamd.OBJ_PLANE, flat(), list(nv) + [u(-9, 9)])
     for _ in range(int(rng.integers(1, 3))):
-        b.obj(fsamd.OBJ_DISC, pick(), p() + n() + [u(0.5, 4)])
+        b.obj(fsamd.OBJ_DISC, flat(), p() + n() + [u(0.5, 4)])
     for _ in range(int(rng.integers(1, 3))):
-        b.obj(fsamd.OBJ_QUAD_ONWH, pick(), p() + n() + [u(1, 6), u(1, 6)])
+        b.obj(fsamd.OBJ_QUAD_ONWH, flat(), p() + n() + [u(1, 6), u(1, 6)])
     for _ in range(int(rng.integers(1, 3))):
-        b.obj(fsamd.OBJ_QUAD_PUV, pick(), p() + [u(-4, 4) for _ in range(6)])
+        b.obj(fsamd.OBJ_QUAD_PUV, flat(), p() + [u(-4, 4) for _ in range(6)])
     for _ in range(int(rng.integers(1, 3))):
-        b.obj(fsamd.OBJ_CUBOID, pick(), p() + [u(0.5, 4), u(0.5, 4), u(0.5, 4)] + n() + [u(-3, 3)],
+        b.obj(fsamd.OBJ_CUBOID, flat(), p() + [u(0.5, 4), u(0.5, 4), u(0.5, 4)] + n() + [u(-3, 3)],
               rotate=int(rng.integers(0, 2)))
     for _ in range(int(rng.integers(2, 4))):  # small meshes: random faces, some sharing an edge
         nf = int(rng.integers(2, 15))
@@ -63,24 +69,26 @@ def random_scene(seed, cloud_tris=3000, crowd=0):
         v = c + rng.normal(scale=u(0.5, 3), size=(nf + 2, 3))
         faces = [[0, 1, i + 2] if rng.random() < 0.3 else list(rng.choice(nf + 2, 3, replace=False))
                  for i in range(nf)]
-        b.mesh(pick(), v.tolist(), faces)
+        b.mesh(flat(), v.tolist(), faces)
     for j in range(crowd):  # many small analytic objects (the object-octree threshold is 182)
         k = int(rng.integers(4))
         if k == 0:
             b.obj(fsamd.OBJ_SPHERE, pick(), p() + [u(0.2, 0.9)])
         elif k == 1:
-            b.obj(fsamd.OBJ_CUBOID, pick(), p() + [u(0.3, 1.2), u(0.3, 1.2), u(0.3, 1.2)] + n() + [u(-3, 3)],
+            b.obj(fsamd.OBJ_CUBOID, flat(), p() + [u(0.3, 1.2), u(0.3, 1.2), u(0.3, 1.2)] + n() + [u(-3, 3)],
                   rotate=1)
         elif k == 2:
-            b.obj(fsamd.OBJ_DISC, pick(), p() + n() + [u(0.3, 1.0)])
+            b.obj(fsamd.OBJ_DISC, flat(), p() + n() + [u(0.3, 1.0)])
         else:
-            b.obj(fsamd.OBJ_QUAD_PUV, pick(), p() + [u(-1, 1) for _ in range(6)])
+            b.obj(fsamd.OBJ_QUAD_PUV, flat(), p() + [u(-1, 1) for _ in range(6)])
     # a triangle cloud for the BVH walk: small faces around random centres
     c = np.array(p())
     centres = c + rng.normal(scale=3.0, size=(cloud_tris, 1, 3))
     tv = (centres + rng.normal(scale=0.35, size=(cloud_tris, 3, 3))).reshape(-1, 3)
-    b.mesh(pick(), tv.tolist(), np.arange(3 * cloud_tris).reshape(-1, 3).tolist(),
-           rotation=(0, 1, 0, u(-1, 1)), scale=(u(0.7, 1.3),) * 3)
+    faces = np.arange(3 * cloud_tris).reshape(-1, 3)
+    tc = rng.random((3 * cloud_tris, 2)) * 4.0 - 1.0 if textured else None
+    b.mesh(flat(), tv.tolist(), faces.tolist(), rotation=(0, 1, 0, u(-1, 1)), scale=(u(0.7, 1.3),) * 3,
+           texcoords=tc, corner_tex=faces if textured else None)
     return b
 
 
@@ -125,5 +133,18 @@ def test_random_crowd_bit_exact(optimized, seed, gpu_renderer):
     out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
     k = gpu_renderer.last_kernel()
     assert (k[:-1].split(", ")[5] == "true") == optimized, k
+    ref = oracle_render(ptr, cam, 80, 60, 8)
+    assert_parity(out, ref, exact=True)
+
+
+@pytest.mark.parametrize("seed", [400, 401, 402])
+def test_random_textured_scene_bit_exact(seed, gpu_renderer):
+    """Random diffuse maps on planes, discs, quads, cuboids and meshes (planar
+    maps and mesh texcoords, material.cpp:108-126): the textured kernel."""
+    b = random_scene(seed, cloud_tris=1000, textured=True)
+    ptr = b.build()
+    cam = CAMS[seed % 2]
+    out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    assert gpu_renderer.last_kernel()[:-1].split(", ")[2] == "true", gpu_renderer.last_kernel()  # TEX
     ref = oracle_render(ptr, cam, 80, 60, 8)
     assert_parity(out, ref, exact=True)
