@@ -148,3 +148,14 @@ def test_random_textured_scene_bit_exact(seed, gpu_renderer):
     assert gpu_renderer.last_kernel()[:-1].split(", ")[2] == "true", gpu_renderer.last_kernel()  # TEX
     ref = oracle_render(ptr, cam, 80, 60, 8)
     assert_parity(out, ref, exact=True)
+
+
+@pytest.mark.parametrize("seed", [500, 501])
+def test_random_scene_larger_frame_bit_exact(seed, gpu_renderer):
+    """Two random scenes at 256 x 192 x 16 spp (790 k samples each)."""
+    b = random_scene(seed)
+    ptr = b.build()
+    cam = CAMS[seed % 2]
+    out = gpu_render(gpu_renderer, ptr, cam, 256, 192, 16)
+    ref = oracle_render(ptr, cam, 256, 192, 16)
+    assert_parity(out, ref, exact=True)
