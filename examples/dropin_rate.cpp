@@ -27,6 +27,10 @@ int main(int argc, char** argv) {
   base::Camera camera;
   if (scene.GetCameraCount()) camera = *scene.GetCamera(0);
   const unsigned W = std::atoi(argv[2]), H = std::atoi(argv[3]), frames = std::atoi(argv[4]);
+  if (W < 2 || H < 2 || frames == 0) {
+    std::fprintf(stderr, "width and height must be >= 2 and frames > 0\n");
+    return 2;
+  }
   base::DisplayFrame frame(W, H);
   base::TraceScene(camera, &scene, &frame);  // upload + BVH build, not timed
   frame.GetDisplayBuffer();
@@ -39,6 +43,10 @@ int main(int argc, char** argv) {
   for (unsigned i = 0; i < frames; i++) {
     base::TraceScene(camera, &scene, &frame);
     frame.GetDisplayBuffer();
+    if (base::LastTraceStatus() != 0) {  // a failed frame must not count as rendered
+      std::fprintf(stderr, "frame %u failed: %s\n", i, base::LastTraceError());
+      return 1;
+    }
   }
   const double loop_s = now_s() - t0;
   // the same samples in one submission, one display read

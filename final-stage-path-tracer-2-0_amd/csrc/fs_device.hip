@@ -19,6 +19,7 @@
 
 #include "fs_bvh_gpu.h"
 #include "fs_kernels.h"
+#include "fs_libm.h"
 #include "fs_scene.h"
 #include "fs_trace.h"
 
@@ -424,6 +425,11 @@ __device__ __forceinline__ f3 random_reflection(const DevScene& S, f3 inc, f3 n,
   if (dot(refl, n) < 0.0f) refl = refl * -1.0f;
   return refl;
 }
+// TRIG: the host libm's cosf/sinf bits (fs_libm.h); without it ocml's, in
+// kernels whose scenes never reach the rotation (no frosted glass) and whose
+// registers are then spent as before (the restatement's double constants cost
+// C3/C4 1 %, profiles/r06/ab_trig.log).
+template <bool TRIG>
 __device__ __forceinline__ f3 random_refraction(const DevScene& S, f3 inc, f3 n, float solid, float index,
                                                 uint64_t& rng) {
   float half = solid / 2.0f;
@@ -434,7 +440,14 @@ __device__ __forceinline__ f3 random_refraction(const DevScene& S, f3 inc, f3 n,
   if (dot(axis, n) < 0.0f) axis = axis * -1.0f;
   if (cmp_eps(solid, kPi, kEpsilon)) return axis;
   if (cmp_eps(solid, 0.0f, kEpsilon)) return refl;
-  return rotate(refl, cosf(delta), sinf(delta), axis);
+  float sn, cs;
+  if (TRIG) {
+    libm::sincosf(delta, &sn, &cs);  // the host libm's cosf / sinf bits (fs_libm.h)
+  } else {
+    cs = cosf(delta);
+    sn = sinf(delta);
+  }
+  return rotate(refl, cs, sn, axis);
 }
 
 // Ceramic's specular term (float)pow((double)(h.n), 50) (material.cpp:280).
@@ -458,6 +471,7 @@ __device__ __forceinline__ float pow50(float xf) {
 // the lanes whose material draws, and two selects; the lanes of a mixed
 // wave then run ONE random_reflection together, with each kind's RNG draws
 // in their order.
+template <bool TRIG>
 __device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_material& m, uint32_t mi, f3 view, f3 n,
                                              uint64_t& rng) {
   const float4 rm = S.rmat[mi];
@@ -470,7 +484,7 @@ __device__ __forceinline__ f3 mat_reflection(const DevScene& S, const fs_materia
   if (mode == kReflScatter) return random_reflection(S, view, n, solid, rng);
   if (mode == kReflMirror) return reflect(view, n);
   if (mode == kReflRefract) return refract(view, n, m.index);
-  if (mode == kReflFrosted) return random_refraction(S, view, n, kPi * m.frost, m.index, rng);
+  if (mode == kReflFrosted) return random_refraction<TRIG>(S, view, n, kPi * m.frost, m.index, rng);
   if (mode == kReflView) return view;
   return mk3(0, 0, 0);
 }
@@ -524,6 +538,7 @@ struct MatTrail {
 };
 
 // engine.cpp:210-244: jittered ray through the pixel, optional thin lens.
+template <bool TRIG>
 __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy, uint64_t& rng) {
   float jx = (float)((double)rng_float(rng) - 0.5);
   float jy = (float)((double)rng_float(rng) - 0.5);
@@ -540,7 +555,14 @@ __device__ __forceinline__ Ray camera_ray(const DevCamera& C, float fx, float fy
     if (ray_plane(C.focal, r, ft, fp)) {
       float ang = (float)((double)rng_float(rng) * 2.0 * (double)kPi);
       float mag = fsqrt(rng_float(rng)) * C.aperture;
-      f3 off = C.right * cosf(ang) * mag + C.up * sinf(ang) * mag;
+      float sn, cs;
+      if (TRIG) {
+        libm::sincosf(ang, &sn, &cs);  // the host libm's cosf / sinf bits (fs_libm.h)
+      } else {  // never reached: the host picks TRIG kernels for cameras with a lens
+        cs = cosf(ang);
+        sn = sinf(ang);
+      }
+      f3 off = C.right * cs * mag + C.up * sn * mag;
       r.start = r.start + off;
       r.stop = r.start + normalize(fp - r.start) * C.z_far;
       r.dir = r.stop - r.start;
@@ -978,7 +1000,13 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       const bool swap = e1 < e0;
       const uint32_t near = swap ? Cw.y : Cw.x, far = swap ? Cw.x : Cw.y;
       const bool any = (swap ? e1 : e0) < kMissT, both = (swap ? e0 : e1) < kMissT;
-      stk[sp * kBlock] = far;  // a push only when both are hit (sp + 1 below); else above the top
+      // A push only when both are hit (sp + 1 below); else a write above the
+      // top. Unconditional, so in bounds only because sp <= this node's depth
+      // < kTraversalStack: both builders stop splitting at depth
+      // kTraversalStack - 1 (fs_scene.cpp split depth rule, kGuard in
+      // fs_bvh_gpu.hip; tests/test_gpu_bvh.py deep-mesh case).
+      static_assert(kTraversalStack >= 2, "the walk stack holds the root's far child");
+      stk[sp * kBlock] = far;
       const uint32_t w1 = any ? near : (sp > 0 ? top1 : kNone);
       const uint32_t sp1 = both ? sp + 1 : (any ? sp : (sp > 0 ? sp - 1 : 0u));
       // Park the first leaf and keep walking from the entry under it: far
@@ -1008,7 +1036,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
     // 1+2 triangles costs the wave 3 trips, not max-per-leaf 2+2. (Selects for
     // this step and a branch-free triangle test with the (t, face) key, as the
     // node step and the small-mesh faces, measured C4 -3 %, C3 -5 %: round 5,
-    // profiles/r05/ab_spills_leaf.log.)
+    // profiles/r05/ab_leafstep.log.)
     while (leaf) {
 #ifdef FS_PHASE_PROF
       FS_WAVE_TRIP(tally.leaf_trips);
@@ -1438,9 +1466,9 @@ __device__ __forceinline__ void planar_tc(f3 p, f3 n, float& u, float& v) {
   }
 }
 // sphere_map_texcoords: float atan2 overload, float BASE_PI, double +0.5/*0.5/1.0-.
-// atan2f is ocml's here and the C runtime's in the reference (tolerance).
+// atan2f is the host C library's (fs_libm.h restatement), bit for bit.
 __device__ __forceinline__ void sphere_tc(f3 n, float& u, float& v) {
-  float uu = (float)((double)(atan2f(n.x, n.z) / (2 * kPi)) + 0.5);
+  float uu = (float)((double)(libm::atan2f(n.x, n.z) / (2 * kPi)) + 0.5);  // fs_libm.h
   float vv = (float)((double)n.y * 0.5 + 0.5);
   u = uu;
   v = (float)(1.0 - (double)vv);
@@ -1693,7 +1721,7 @@ __device__ __forceinline__ uint32_t fetch_block(const Launch& P, uint32_t* __res
 //
 // NOWALK (every mesh small): no walk stack and 8 waves per SIMD.
 template <bool COUNT, int WAVES, bool TEX = false, bool SUSP = false, bool MMAT = false, bool SOCT = false,
-          bool NOWALK = false>
+          bool NOWALK = false, bool TRIG = false>
 __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, DevCamera C, DevFrame F, Launch P,
                                                                     PathRecords R,
                                                                     float4* __restrict__ anchor_all,
@@ -1726,6 +1754,13 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   bool fresh = true;
   MinHit h;         // persists across iterations while a walk is parked (SUSP)
   WalkSuspend ws;
+#ifdef FS_WAVE_TIMES
+  // measurement build (libfsgpu_wt.so): when the wave starts, first finds
+  // every queue empty and ends (s_memrealtime, 100 MHz), iterations after that
+  const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
+  uint64_t wt_drain = 0, wt_iters = 0, wt_drain_iter = 0;
+  if (lane == 0) atomicMax(&counters->phase[31], ~wt_start);  // ~ the earliest start
+#endif
 #ifdef FS_PHASE_PROF
   uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t seqc[2] = {0, 0};  // PhaseAcc::seq / chain summed over this wave's trace calls
@@ -1759,6 +1794,12 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         if (cur.next >= cur.total) {
           const uint32_t z = cur.sample0 >> 31;  // 0 (sample indices stay below 2^20)
           const uint32_t b = fetch_block(at_use(P, z), queues, queue, queues_left);
+#ifdef FS_WAVE_TIMES
+          if (b == kNoBlock && !wt_drain) {
+            wt_drain = __builtin_amdgcn_s_memrealtime();
+            wt_drain_iter = wt_iters;
+          }
+#endif
           if (b == kNoBlock) break;
           cur = decode_block(at_use(P, z), at_use(F, z), b);
         } else {
@@ -1792,7 +1833,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
     }
     if (fresh) {
       rng = pixel_seed(pix, smp, at_use(P, cur.sample0 >> 31).seed);
-      r = camera_ray(at_use(C, cur.sample0 >> 31), (float)x, (float)y, rng);
+      r = camera_ray<TRIG>(at_use(C, cur.sample0 >> 31), (float)x, (float)y, rng);
       depth = 0;
       mats.reset();
       top = -1;
@@ -1859,7 +1900,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         }
         int32_t kind = m.kind;
         f3 view = normalize(p - r.start);
-        f3 refl = mat_reflection(S, m, (uint32_t)mi, view, nn, rng);
+        f3 refl = mat_reflection<TRIG>(S, m, (uint32_t)mi, view, nn, rng);
         float c = fmaxf(0.0f, dot(nn, refl));
         float ds = 0.0f;
         if (kind == FS_MAT_CERAMIC || kind == FS_MAT_GLOW) {
@@ -1925,7 +1966,26 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
 #ifdef FS_PHASE_PROF
     ph[8]++;
 #endif
+#ifdef FS_WAVE_TIMES
+    wt_iters++;
+#endif
   }
+#ifdef FS_WAVE_TIMES
+  {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x)) {
+      const uint64_t base = ~atomicOr(&counters->phase[31], 0ull);
+      const uint64_t bin = 20000;  // 200 us
+      if (!wt_drain) wt_drain = t_end;
+      const uint64_t be = (t_end - base) / bin, bd = (wt_drain - base) / bin;
+      atomicAdd(&counters->phase[be < 13 ? be : 13], 1ull);
+      atomicAdd(&counters->phase[14 + (bd < 13 ? bd : 13)], 1ull);
+      atomicAdd(&counters->phase[28], (unsigned long long)(t_end - wt_drain));
+      atomicMax(&counters->phase[29], (unsigned long long)(t_end - wt_drain));
+      atomicAdd(&counters->phase[30], (unsigned long long)(wt_iters - wt_drain_iter));
+    }
+  }
+#endif
 #ifdef FS_PHASE_PROF
   ph[9] = __builtin_readcyclecounter() - t_begin;
   if (lane == 0) {
@@ -2287,6 +2347,29 @@ struct DevBuf {
   }
 };
 
+// The lookahead of a 1-spp-style render (fs_options.lookahead): the next
+// call's samples traced in the background on a stream of their own, into
+// their own path records, anchor rows, queues and AOV planes, two slots used
+// in turn so one slot's trace can start while the other's drains.
+constexpr uint32_t kLookaheadSpp = 4;
+struct LookKey {  // everything a lookahead trace depends on
+  fs_camera camera;
+  fs_render_params params;  // sample_base: the first sample it traces
+  fs_options opt;
+  uint64_t scene_gen;
+};
+struct Lookahead {
+  hipStream_t stream[2] = {nullptr, nullptr};
+  hipEvent_t traced[2] = {}, folded[2] = {}, order = nullptr, kev0[2] = {}, kev1[2] = {};
+  DevBuf rows[2], aov[2], queues[2];
+  bool pending[2] = {false, false};
+  bool folded_valid[2] = {false, false};  // folded[i] recorded: the last fold that read slot i
+  LookKey key[2];
+  Launch L[2];
+  PathRecords R[2];
+  int next = 0;
+};
+
 }  // namespace
 
 struct fs_context {
@@ -2303,6 +2386,7 @@ struct fs_context {
   bool has_parking = false;  // a mesh of >= park_min_tris triangles: the PARKED schedule
   bool has_walks = false;    // a mesh with a BVH (not small): the kernel needs the walk stack
   bool many_materials = false;  // > kPackedMaterials: material ids in scratch rows (MMAT kernels)
+  bool has_frost = false;  // a Glass of frost != 0: its refraction rotates by cosf/sinf (TRIG kernels)
   const char* last_kernel = "";  // the trace kernel the last fs_render launched
   std::vector<uint32_t> tile_order_host;  // the device tile_order buffer holds this order of ...
   uint64_t tile_order_key[3] = {0, 0, 0};  // ... the tile set (offset, stride, owned; width, height) it was built for
@@ -2320,12 +2404,16 @@ struct fs_context {
   DevBuf rows;  // the Fog anchor rows and the path records of a render (path_records)
   DevBuf queues;  // per-XCD work-queue counters of the persistent trace kernel
   uint32_t cus = 0;  // compute units: the persistent grid is one wave per wave slot
+  uint64_t scene_gen = 0;  // uploads so far (a lookahead is of one upload)
+  Lookahead la;
+  int last_spec = -1;  // the lookahead slot the last fs_render folded, or -1
 };
 
 struct fs_frame {
   fs_context* ctx = nullptr;
   uint32_t width = 0, height = 0;
   DevBuf color, count, display, normal, depth, material;
+  void* pinned[FS_PLANE_MATERIAL + 1] = {};  // fs_frame_map's page-locked copies
 };
 
 namespace {
@@ -2401,9 +2489,14 @@ DevCamera camera_basis(const fs_camera* c, uint32_t W, uint32_t H) {
 size_t record_bytes(bool tex, bool mmat) {
   return 8 * kMaxDepth + 16 + (mmat ? 4 * kMaxDepth : 8) + (tex ? 16 * kMaxDepth : 0);
 }
+size_t rows_bytes(uint64_t wave_lanes, uint64_t samples, bool tex, bool mmat) {
+  return (size_t)wave_lanes * 32 + (size_t)samples * record_bytes(tex, mmat) + 6 * 256;  // + alignment
+}
+int carve_records(DevBuf* rows, uint64_t wave_lanes, uint64_t samples, PathRecords* R, float4** anchors, bool tex,
+                  bool mmat);
 int path_records(fs_context* ctx, uint64_t wave_lanes, uint64_t samples, PathRecords* R, float4** anchors, bool tex,
                  bool mmat) {
-  const size_t bytes = (size_t)wave_lanes * 32 + (size_t)samples * record_bytes(tex, mmat) + 6 * 256;  // + alignment
+  const size_t bytes = rows_bytes(wave_lanes, samples, tex, mmat);
   // Shrink a buffer more than 4x (and 1 GiB) larger than this render needs:
   // a context that once rendered a long launch does not keep its records.
   if (ctx->rows.bytes > 4 * bytes && ctx->rows.bytes - bytes > (1ull << 30)) ctx->rows.release();
@@ -2411,7 +2504,11 @@ int path_records(fs_context* ctx, uint64_t wave_lanes, uint64_t samples, PathRec
     int rc = ensure(&ctx->rows, bytes);
     if (rc) return rc == FS_ERR_DEVICE ? fail(FS_ERR_NOMEM, "path records: " + g_error) : rc;
   }
-  char* p = (char*)ctx->rows.p;
+  return carve_records(&ctx->rows, wave_lanes, samples, R, anchors, tex, mmat);
+}
+int carve_records(DevBuf* rows, uint64_t wave_lanes, uint64_t samples, PathRecords* R, float4** anchors, bool tex,
+                  bool mmat) {
+  char* p = (char*)rows->p;
   auto take = [&](size_t n) {
     char* q = p;
     p += (n + 255) & ~(size_t)255;
@@ -2426,8 +2523,17 @@ int path_records(fs_context* ctx, uint64_t wave_lanes, uint64_t samples, PathRec
   R->mats = mmat ? nullptr : (uint2*)take(8ull * samples);
   R->mat = mmat ? (uint32_t*)take(4ull * kMaxDepth * samples) : nullptr;
   R->tex = tex ? (float4*)take(16ull * kMaxDepth * samples) : nullptr;
-  if ((size_t)(p - (char*)ctx->rows.p) > ctx->rows.bytes) return fail(FS_ERR_NOMEM, "path record overflow");
+  if ((size_t)(p - (char*)rows->p) > rows->bytes) return fail(FS_ERR_NOMEM, "path record overflow");
   return FS_OK;
+}
+
+// Waits for every lookahead trace of the context and drops them (before the
+// scene, the tile order or the context they read is replaced or freed).
+void la_quiesce(fs_context* ctx) {
+  for (int i = 0; i < 2; i++) {
+    if (ctx->la.stream[i]) (void)hipStreamSynchronize(ctx->la.stream[i]);
+    ctx->la.pending[i] = false;
+  }
 }
 
 size_t plane_bytes(int plane, size_t pixels) {
@@ -2516,29 +2622,40 @@ struct LeanKernel {
   const char* name;
   uint32_t waves;  // waves per SIMD (__launch_bounds__)
 };
-template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false>
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false, bool TRIG = false>
 LeanKernel lean_kernel(bool count) {
   constexpr int W = SUSP ? kSuspWaves : NOWALK ? kNowalkWaves : kLeanWaves;
   static const std::string name = std::string("render_kernel_lean<false, ") + std::to_string(W) + ", " +
                                   (TEX ? "true" : "false") + ", " + (SUSP ? "true" : "false") + ", " +
                                   (MMAT ? "true" : "false") + ", " + (SOCT ? "true" : "false") + ", " +
-                                  (NOWALK ? "true>" : "false>");
-  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK>
-                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK>,
+                                  (NOWALK ? "true" : "false") + ", " + (TRIG ? "true>" : "false>");
+  return {count ? (LeanFn)dev::render_kernel_lean<true, W, TEX, SUSP, MMAT, SOCT, NOWALK, TRIG>
+                : (LeanFn)dev::render_kernel_lean<false, W, TEX, SUSP, MMAT, SOCT, NOWALK, TRIG>,
           name.c_str(), (uint32_t)W};
+}
+template <bool TEX, bool SUSP, bool MMAT, bool SOCT = false, bool NOWALK = false>
+LeanKernel lean_kernel(bool count, bool trig) {
+  return trig ? lean_kernel<TEX, SUSP, MMAT, SOCT, NOWALK, true>(count)
+              : lean_kernel<TEX, SUSP, MMAT, SOCT, NOWALK, false>(count);
 }
 // Scenes traced through the object octree take one instantiation that covers
 // textures and any material count (their object loop is per lane anyway).
 // Untextured scenes whose meshes are all small (no BVH walk) take the NOWALK
-// instantiation: no walk stack, shading rows in LDS.
-LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks) {
-  if (object_tree) return lean_kernel<true, false, true, true>(count);
-  if (tex) return many_materials ? lean_kernel<true, false, true>(count) : lean_kernel<true, false, false>(count);
-  if (parked) return many_materials ? lean_kernel<false, true, true>(count) : lean_kernel<false, true, false>(count);
+// instantiation: no walk stack, shading rows in LDS. trig: the host libm's
+// sinf/cosf for a thin-lens camera or frosted glass (TRIG; textured kernels
+// always, for their sphere maps' atan2f too).
+LeanKernel pick_kernel(bool count, bool tex, bool parked, bool many_materials, bool object_tree, bool walks,
+                       bool trig) {
+  if (object_tree) return lean_kernel<true, false, true, true, false, true>(count);
+  if (tex)
+    return many_materials ? lean_kernel<true, false, true, false, false, true>(count)
+                          : lean_kernel<true, false, false, false, false, true>(count);
+  if (parked)
+    return many_materials ? lean_kernel<false, true, true>(count, trig) : lean_kernel<false, true, false>(count, trig);
   if (!walks)
-    return many_materials ? lean_kernel<false, false, true, false, true>(count)
-                          : lean_kernel<false, false, false, false, true>(count);
-  return many_materials ? lean_kernel<false, false, true>(count) : lean_kernel<false, false, false>(count);
+    return many_materials ? lean_kernel<false, false, true, false, true>(count, trig)
+                          : lean_kernel<false, false, false, false, true>(count, trig);
+  return many_materials ? lean_kernel<false, false, true>(count, trig) : lean_kernel<false, false, false>(count, trig);
 }
 
 bool valid_options(const fs_options* o, std::string* why) {
@@ -2552,6 +2669,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
   else if (o->park_lanes > 64 || o->park_lanes_small > 64) *why = "park_lanes must be 0..64";
   else if (o->lds_rows > 1) *why = "lds_rows must be 0 or 1";
+  else if (o->lookahead > 1) *why = "lookahead must be 0 or 1";
   else return true;
   return false;
 }
@@ -2596,7 +2714,9 @@ struct Plan {
 int make_plan(uint32_t owned, uint32_t mpt, uint32_t spp, const fs_options& O, uint64_t budget, size_t rec_bytes,
               Plan* out) {
   Plan p;
-  p.chunk = O.samples_per_block;
+  // a launch of fewer samples than a block holds sizes its records to spp
+  // (the 1-spp drop-in loop: no 16x over-allocation)
+  p.chunk = std::min<uint32_t>(O.samples_per_block, std::max<uint32_t>(spp, 1));
   p.tiles = owned;
   const uint64_t cap = budget / rec_bytes;          // path records one launch may hold
   const uint64_t tile_samples = (uint64_t)mpt * kBlock;  // one sample of each pixel of one tile
@@ -2688,8 +2808,17 @@ int fs_create(int device, fs_context** out) {
 int fs_destroy(fs_context* ctx) {
   if (!ctx) return FS_OK;
   (void)hipSetDevice(ctx->device);
+  la_quiesce(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (int i = 0; i < 2; i++) {
+    Lookahead& A = ctx->la;
+    for (DevBuf* b : {&A.rows[i], &A.aov[i], &A.queues[i]}) b->release();
+    for (hipEvent_t e : {A.traced[i], A.folded[i], A.kev0[i], A.kev1[i]})
+      if (e) (void)hipEventDestroy(e);
+    if (A.stream[i]) (void)hipStreamDestroy(A.stream[i]);
+  }
+  if (ctx->la.order) (void)hipEventDestroy(ctx->la.order);
   for (DevBuf* b : {&ctx->objects, &ctx->nodes, &ctx->tris, &ctx->tri_normals, &ctx->tri_tex, &ctx->tree, &ctx->tree_objs,
                     &ctx->tex_rgb, &ctx->tex_info, &ctx->materials, &ctx->umat, &ctx->rmat, &ctx->table, &ctx->range_io,
                     &ctx->counters, &ctx->pack_send, &ctx->pack_recv, &ctx->tile_order, &ctx->queues})
@@ -2724,6 +2853,7 @@ int fs_options_default(fs_options* o) {
   o->build_log = 0;
   o->persist = 1;
   o->small_mesh_tris = 16;
+  o->lookahead = 1;
   return FS_OK;
 }
 
@@ -2758,6 +2888,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
   int rc = prepare_scene(desc, &P, &err, bo, gpu_min);
   if (rc) return fail(rc, err);
   if ((rc = set_device(ctx))) return rc;
+  la_quiesce(ctx);  // lookahead traces read the scene this upload replaces
+  ctx->scene_gen++;
   auto t0 = std::chrono::steady_clock::now();
   ctx->have_scene = false;
   if ((rc = upload(ctx, &ctx->objects, P.objects.data(), P.objects.size() * sizeof(DevObject)))) return rc;
@@ -2893,6 +3025,8 @@ int fs_upload_scene_ex(fs_context* ctx, const fs_scene_desc* desc, uint32_t flag
     ctx->has_walks |= o.kind == FS_OBJ_MESH && o.i2 && !o.i3;
   }
   ctx->many_materials = P.materials.size() > kPackedMaterials;
+  ctx->has_frost = false;
+  for (const fs_material& m : P.materials) ctx->has_frost |= m.kind == FS_MAT_GLASS && m.frost != 0.0f;
   ctx->num_objects = S.num_objects;
   ctx->host = std::move(P);
   ctx->have_scene = true;
@@ -2942,8 +3076,24 @@ int fs_frame_destroy(fs_frame* f) {
   if (!f) return FS_OK;
   (void)hipSetDevice(f->ctx->device);
   (void)hipStreamSynchronize(f->ctx->stream);
-  for (int pl = FS_PLANE_COLOR; pl <= FS_PLANE_MATERIAL; pl++) plane_buf(f, pl)->release();
+  for (int pl = FS_PLANE_COLOR; pl <= FS_PLANE_MATERIAL; pl++) {
+    plane_buf(f, pl)->release();
+    if (f->pinned[pl]) (void)hipHostFree(f->pinned[pl]);
+  }
   delete f;
+  return FS_OK;
+}
+
+int fs_frame_map(fs_frame* f, int plane, const void** host) {
+  if (!f || !host) return fail(FS_ERR_INVALID, "null argument");
+  DevBuf* b = plane_buf(f, plane);
+  if (!b) return fail(FS_ERR_INVALID, "unknown plane");
+  int rc;
+  if ((rc = set_device(f->ctx))) return rc;
+  if (!f->pinned[plane]) FS_HIP(hipHostMalloc(&f->pinned[plane], b->bytes, hipHostMallocDefault));
+  FS_HIP(hipMemcpyAsync(f->pinned[plane], b->p, b->bytes, hipMemcpyDeviceToHost, f->ctx->stream));
+  FS_HIP(hipStreamSynchronize(f->ctx->stream));
+  *host = f->pinned[plane];
   return FS_OK;
 }
 
@@ -3042,39 +3192,33 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   if ((rc = make_plan(owned, mpt, params->spp, O, row_budget, rec_bytes, &plan))) return rc;
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
+  ctx->last_spec = -1;
   PathRecords rec;
   float4* anchors = nullptr;
   const LeanKernel K = pick_kernel(count, ctx->has_textures, parked, mm, ctx->scene.tree != nullptr,
-                                   ctx->has_walks || !O.lds_rows);
+                                   ctx->has_walks || !O.lds_rows, C.aperture > 0.0f || ctx->has_frost);
   // The persistent grid: one wave per wave slot of the chip (4 SIMDs per CU,
   // K.waves waves per SIMD), never more than the launch has blocks.
   const uint64_t wave_slots = (uint64_t)ctx->cus * 4u * K.waves;
   auto grid_for = [&](uint64_t nb) { return O.persist ? std::min<uint64_t>(wave_slots, nb) : nb; };
-  // On an allocation failure the launches shrink (groups per launch, then
-  // tiles per part, then samples per block, each halved) until the records fit.
-  while (blocks) {
-    const uint64_t pb = (uint64_t)plan.tiles * mpt;  // blocks of the largest part
-    if (!(rc = path_records(ctx, grid_for(pb * plan.G) * kBlock, pb * plan.G * plan.chunk * kBlock, &rec, &anchors,
-                            tex_rec, mm)))
-      break;
-    if (O.groups || !plan.shrink(owned)) return rc;
-    (void)hipGetLastError();  // clear the failed hipMalloc's error state
-  }
   ctx->last_kernel = K.name;
   L.persist = O.persist;
   L.groups = 1;
   L.group_major = O.group_major;
   L.tile_order = nullptr;
+  bool order_copied = false;  // the tile order was (re)written on the context stream by this call
   // Longest jobs first: tiles nearer the image centre (where the scenes put
   // their geometry) are dispatched first, so the launch tail runs on cheap
   // edge tiles. Ties keep index order. Only the dispatch order changes: every
   // tile keeps its path records. (A render in several tile parts dispatches
   // each part in index order.)
   if (owned > 1 && O.tile_order && plan.parts == 1) {
-    const uint64_t key[3] = {((uint64_t)L.tile_offset << 32) | L.tile_stride, owned,
-                             ((uint64_t)params->width << 32) | params->height};
+    const uint64_t okey[3] = {((uint64_t)L.tile_offset << 32) | L.tile_stride, owned,
+                              ((uint64_t)params->width << 32) | params->height};
     std::vector<uint32_t>& ord = ctx->tile_order_host;
-    if (!std::equal(key, key + 3, ctx->tile_order_key)) {
+    if (!std::equal(okey, okey + 3, ctx->tile_order_key)) {
+      la_quiesce(ctx);  // a lookahead may read the old order
+      order_copied = true;
       ord.resize(owned);
       std::vector<float> dist(owned);
       const float cx = 0.5f * (float)params->width, cy = 0.5f * (float)params->height;
@@ -3089,10 +3233,41 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       if ((rc = ensure(&ctx->tile_order, owned * sizeof(uint32_t)))) return rc;
       FS_HIP(hipMemcpyAsync(ctx->tile_order.p, ord.data(), owned * sizeof(uint32_t), hipMemcpyHostToDevice,
                             ctx->stream));
-      std::copy(key, key + 3, ctx->tile_order_key);
+      std::copy(okey, okey + 3, ctx->tile_order_key);
     }
     L.tile_order = (const uint32_t*)ctx->tile_order.p;
   }
+  // Lookahead (fs_options.lookahead): a whole-frame render of at most
+  // kLookaheadSpp samples in one launch. A pending lookahead of exactly this
+  // call is folded instead of tracing; every other one is dropped (its stream
+  // may still run: it writes only its own slot).
+  Lookahead& A = ctx->la;
+  const bool la_ok = O.lookahead && !count && stride == 1 && params->tile_offset == 0 && O.persist && blocks &&
+                     params->spp <= kLookaheadSpp && plan.parts == 1 && plan.G == 1 && plan.chunk == params->spp;
+  LookKey key;
+  std::memset(&key, 0, sizeof key);
+  int hit = -1;
+  if (la_ok) {
+    key.camera = *camera;
+    key.params = *params;
+    key.opt = O;
+    key.scene_gen = ctx->scene_gen;
+    for (int i = 0; i < 2; i++)
+      if (A.pending[i] && !std::memcmp(&A.key[i], &key, sizeof key)) hit = i;
+  }
+  for (int i = 0; i < 2; i++)
+    if (i != hit) A.pending[i] = false;
+  // On an allocation failure the launches shrink (groups per launch, then
+  // tiles per part, then samples per block, each halved) until the records fit.
+  while (blocks && hit < 0) {
+    const uint64_t pb = (uint64_t)plan.tiles * mpt;  // blocks of the largest part
+    if (!(rc = path_records(ctx, grid_for(pb * plan.G) * kBlock, pb * plan.G * plan.chunk * kBlock, &rec, &anchors,
+                            tex_rec, mm)))
+      break;
+    if (O.groups || !plan.shrink(owned)) return rc;
+    (void)hipGetLastError();  // clear the failed hipMalloc's error state
+  }
+  if (plan.parts != 1) L.tile_order = nullptr;  // shrunk into tile parts: index order
   const bool lm = ctx->scene.num_materials <= dev::kFoldLdsMaterials;
   const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
   const FoldFn fold = pick_fold(tex_rec, mm, lm);
@@ -3101,7 +3276,32 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // fold kernel's resident wave slots at least twice over, else 2 or 4 (a
   // rank's share of a multi-GPU frame), so the serial per-pixel loop is split.
   const uint64_t fold_slots = (uint64_t)ctx->cus * fold_waves_per_cu(fold, fold_lds);
-  for (uint32_t part = 0; part < plan.parts; part++) {
+  if (hit >= 0) {
+    // The lookahead traced exactly these samples: its depth-0 AOVs into the
+    // frame, then the fold of its records, after its trace on the other stream.
+    const size_t px = (size_t)frame->width * frame->height;
+    FS_HIP(hipStreamWaitEvent(ctx->stream, A.traced[hit], 0));
+    FS_HIP(hipMemcpyAsync(frame->normal.p, A.aov[hit].p, 12 * px, hipMemcpyDeviceToDevice, ctx->stream));
+    FS_HIP(hipMemcpyAsync(frame->depth.p, (char*)A.aov[hit].p + 12 * px, 4 * px, hipMemcpyDeviceToDevice, ctx->stream));
+    FS_HIP(hipMemcpyAsync(frame->material.p, (char*)A.aov[hit].p + 16 * px, 8 * px, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    const Launch& Lh = A.L[hit];
+    const uint64_t pblocks = (uint64_t)Lh.owned * mpt;
+    const uint32_t fold_log2 = pblocks >= 2 * fold_slots ? 0u : (pblocks >= fold_slots ? 1u : 2u);
+    if (fold_log2 == 0)
+      hipLaunchKernelGGL(fold, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, Lh, A.R[hit]);
+    else
+      hipLaunchKernelGGL(fold_split, dim3((uint32_t)(pblocks << fold_log2)), dim3(kBlock), fold_lds, ctx->stream,
+                         ctx->scene, F, Lh, A.R[hit], fold_log2);
+    FS_HIP(hipGetLastError());
+    FS_HIP(hipEventRecord(A.folded[hit], ctx->stream));
+    A.folded_valid[hit] = true;
+    A.pending[hit] = false;
+    ctx->last_spec = hit;
+    ctx->last_launches = 1;
+    ctx->last_launch_spp = Lh.spp;
+  }
+  for (uint32_t part = 0; part < plan.parts && hit < 0; part++) {
     // part p: the render's owned tiles p * tiles ..., i.e. the frame's tiles
     // tile_offset + (p * tiles + i) * stride
     const uint32_t first = part * plan.tiles;
@@ -3136,6 +3336,62 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         hipLaunchKernelGGL(fold_split, dim3((uint32_t)(pblocks << fold_log2)), dim3(kBlock), fold_lds, ctx->stream,
                            ctx->scene, F, L, rec, fold_log2);
       FS_HIP(hipGetLastError());
+    }
+  }
+  // The next call's samples, traced now in the background (slot s, the one
+  // not just folded), unless they would leave the 2^20-sample seed range.
+  if (la_ok && (uint64_t)params->sample_base + 2ull * params->spp <= (1ull << 20)) {
+    const int s = hit >= 0 ? (hit ^ 1) : A.next;
+    A.next = s ^ 1;
+    const uint64_t pb = (uint64_t)owned * mpt;
+    const uint64_t grid = grid_for(pb);
+    const size_t px = (size_t)frame->width * frame->height;
+    bool ready = true;
+    if (!A.stream[s]) {
+      FS_HIP(hipStreamCreateWithFlags(&A.stream[s], hipStreamNonBlocking));
+      FS_HIP(hipEventCreateWithFlags(&A.traced[s], hipEventDisableTiming));
+      FS_HIP(hipEventCreateWithFlags(&A.folded[s], hipEventDisableTiming));
+      FS_HIP(hipEventCreate(&A.kev0[s]));
+      FS_HIP(hipEventCreate(&A.kev1[s]));
+      if (!A.order) FS_HIP(hipEventCreateWithFlags(&A.order, hipEventDisableTiming));
+    }
+    const size_t need = rows_bytes(grid * kBlock, pb * params->spp * kBlock, tex_rec, mm);
+    if (A.rows[s].bytes < need || A.aov[s].bytes < 24 * px || !A.queues[s].p) {
+      FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace still uses the old buffers
+      ready = !ensure(&A.rows[s], need) && !ensure(&A.aov[s], 24 * px) &&
+              !ensure(&A.queues[s], 8 * dev::kQueueStride * sizeof(uint32_t));
+      if (!ready) (void)hipGetLastError();  // no room: this call has no lookahead
+    }
+    if (ready && !carve_records(&A.rows[s], grid * kBlock, pb * params->spp * kBlock, &A.R[s], &anchors, tex_rec, mm)) {
+      Launch Ls = L;
+      Ls.owned = owned;
+      Ls.tile_offset = 0;
+      Ls.sample_base = params->sample_base + params->spp;
+      Ls.spp = params->spp;
+      Ls.groups = 1;
+      Ls.nblocks = (uint32_t)pb;
+      DevFrame Fs{};  // the trace writes only the last sample's AOVs: into the slot's planes
+      Fs.width = frame->width;
+      Fs.height = frame->height;
+      Fs.normal = (float*)A.aov[s].p;
+      Fs.depth = (float*)((char*)A.aov[s].p + 12 * px);
+      Fs.material = (uint64_t*)((char*)A.aov[s].p + 16 * px);
+      if (A.folded_valid[s]) FS_HIP(hipStreamWaitEvent(A.stream[s], A.folded[s], 0));  // its records' last reader
+      if (order_copied) {
+        FS_HIP(hipEventRecord(A.order, ctx->stream));
+        FS_HIP(hipStreamWaitEvent(A.stream[s], A.order, 0));
+      }
+      FS_HIP(hipMemsetAsync(A.queues[s].p, 0, A.queues[s].bytes, A.stream[s]));
+      FS_HIP(hipEventRecord(A.kev0[s], A.stream[s]));
+      hipLaunchKernelGGL(K.fn, dim3((uint32_t)grid), dim3(kBlock), 0, A.stream[s], ctx->scene, C, Fs, Ls, A.R[s],
+                         anchors, (uint32_t*)A.queues[s].p, (DevCounters*)ctx->counters.p);
+      FS_HIP(hipGetLastError());
+      FS_HIP(hipEventRecord(A.kev1[s], A.stream[s]));
+      FS_HIP(hipEventRecord(A.traced[s], A.stream[s]));
+      A.L[s] = Ls;
+      A.key[s] = key;
+      A.key[s].params.sample_base = Ls.sample_base;
+      A.pending[s] = true;
     }
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));
@@ -3206,6 +3462,11 @@ int fs_last_trace_ms(fs_context* ctx, float* ms) {
   int rc;
   if ((rc = set_device(ctx))) return rc;
   float sum = 0.0f;
+  if (ctx->last_spec >= 0) {  // the last render folded a lookahead: its trace's time
+    FS_HIP(hipEventSynchronize(ctx->la.kev1[ctx->last_spec]));
+    FS_HIP(hipEventElapsedTime(ms, ctx->la.kev0[ctx->last_spec], ctx->la.kev1[ctx->last_spec]));
+    return FS_OK;
+  }
   for (uint32_t i = 0; i < ctx->last_launches; i++) {
     float t = 0.0f;
     FS_HIP(hipEventSynchronize(ctx->kev[2 * i + 1]));
@@ -3213,6 +3474,12 @@ int fs_last_trace_ms(fs_context* ctx, float* ms) {
     sum += t;
   }
   *ms = sum;
+  return FS_OK;
+}
+
+int fs_last_render_lookahead(fs_context* ctx, int* folded) {
+  if (!ctx || !folded) return fail(FS_ERR_INVALID, "null argument");
+  *folded = ctx->last_spec >= 0 ? 1 : 0;
   return FS_OK;
 }
 
@@ -3232,6 +3499,18 @@ int fs_read_counters(fs_context* ctx, fs_counters* out) {
   out->object_loads = c.object_loads;
   out->small_tri_loads = c.small_tri_loads;
   out->lane_object_loads = c.lane_object_loads;
+#ifdef FS_WAVE_TIMES
+  {
+    uint64_t waves = 0;
+    for (int i = 0; i < 14; i++) waves += c.phase[i];
+    std::fprintf(stderr, "[fs waves] %llu waves; end time (200 us bins):", (unsigned long long)waves);
+    for (int i = 0; i < 14; i++) std::fprintf(stderr, " %llu", c.phase[i]);
+    std::fprintf(stderr, "; first empty queues (200 us bins):");
+    for (int i = 14; i < 28; i++) std::fprintf(stderr, " %llu", c.phase[i]);
+    std::fprintf(stderr, "; drain after empty queues: mean %.1f us, max %.1f us, %.1f iterations per wave\n",
+                 c.phase[28] / 100.0 / (waves ? waves : 1), c.phase[29] / 100.0, (double)c.phase[30] / (waves ? waves : 1));
+  }
+#endif
 #ifdef FS_PHASE_PROF
   std::fprintf(stderr,
                "[fs phase] loop-top %llu fresh %llu trace %llu (root-cull %llu mesh-traversal %llu analytic %llu) "

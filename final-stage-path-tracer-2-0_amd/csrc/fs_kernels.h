@@ -102,11 +102,12 @@ struct PathRecords {
   float4* tex;     // [level][q]: SampleDiffuse's texel of a textured material (TEX), else null
   uint64_t n;      // samples of the launch (the level stride)
 };
+// PathRecords::end.w flag: level 0 is Fog and its draw took the diffuse colour
 constexpr uint32_t kRecFogDif = 0x100u;
 // DevScene::rmat.w bits: mode A (bits 0-3), mode B (bits 4-7), and whether
 // the material draws one uniform number first (Glass, Liquid, Ceramic, Glow).
 enum ReflMode : uint32_t { kReflScatter = 0, kReflZero = 1, kReflMirror = 2, kReflRefract = 3, kReflFrosted = 4, kReflView = 5 };
-constexpr uint32_t kReflDraws = 0x100u;  // level 0 is Fog and its draw took the diffuse colour
+constexpr uint32_t kReflDraws = 0x100u;  // rmat.w: the material draws one uniform number first
 
 struct Launch {
   uint32_t tile_size, tiles_x, tile_offset, tile_stride;

@@ -98,7 +98,7 @@ class fs_options(C.Structure):
                 ("bvh_leaf", C.c_uint32), ("bvh_bins", C.c_uint32), ("bvh_threads", C.c_uint32),
                 ("node_layout", C.c_uint32), ("build_log", C.c_uint32),
                 ("persist", C.c_uint32), ("small_mesh_tris", C.c_uint32), ("park_lanes_small", C.c_uint32),
-                ("lds_rows", C.c_uint32), ("record_budget_mb", C.c_uint32)]
+                ("lds_rows", C.c_uint32), ("record_budget_mb", C.c_uint32), ("lookahead", C.c_uint32)]
 
 
 class fs_render_plan(C.Structure):
@@ -131,6 +131,8 @@ GPU_SYMBOLS = {
     "fs_frame_reset": ([_VP], C.c_int),
     "fs_frame_read": ([_VP, C.c_int, _VP, C.c_size_t], C.c_int),
     "fs_frame_write": ([_VP, C.c_int, _VP, C.c_size_t], C.c_int),
+    "fs_frame_map": ([_VP, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "fs_last_render_lookahead": ([_VP, C.POINTER(C.c_int)], C.c_int),
     "fs_render": ([_VP, C.POINTER(fs_camera), C.POINTER(fs_render_params), _VP], C.c_int),
     "fs_synchronize": ([_VP], C.c_int),
     "fs_read_counters": ([_VP, C.POINTER(fs_counters)], C.c_int),
@@ -185,7 +187,7 @@ _host = None
 # Entry points added after ABI 4. A measurement build of an earlier round
 # (tools/lib_ab.sh A/B against an older libfsgpu.so, selected by
 # FSAMD_GPU_LIB) may lack them; the product library always has them.
-_OPTIONAL = {"fs_comm_count", "fs_bvh_quality", "fs_plan_render"}
+_OPTIONAL = {"fs_comm_count", "fs_bvh_quality", "fs_plan_render", "fs_frame_map", "fs_last_render_lookahead"}
 
 
 def _bind(lib, table):
@@ -372,6 +374,16 @@ class Frame:
         _check(gpu_lib().fs_frame_read(self.h, plane, out.ctypes.data, out.nbytes), "fs_frame_read")
         return out
 
+    def map(self, plane):
+        """fs_frame_map: the plane in the frame's page-locked host buffer (a copy
+        of it is returned; the buffer is reused by the next map of the plane)."""
+        dt, ch = _PLANE_DTYPE[plane]
+        shape = (self.height, self.width, ch) if ch > 1 else (self.height, self.width)
+        p = C.c_void_p()
+        _check(gpu_lib().fs_frame_map(self.h, plane, C.byref(p)), "fs_frame_map")
+        n = int(np.prod(shape)) * np.dtype(dt).itemsize
+        return np.frombuffer(C.string_at(p.value, n), dt).reshape(shape).copy()
+
     def write(self, plane, array):
         dt, _ = _PLANE_DTYPE[plane]
         a = np.ascontiguousarray(array, dtype=dt)
@@ -502,6 +514,12 @@ class Renderer:
         n, spp = C.c_uint32(), C.c_uint32()
         _check(gpu_lib().fs_last_render_launches(self.ctx, C.byref(n), C.byref(spp)), "fs_last_render_launches")
         return n.value, spp.value
+
+    def last_lookahead(self):
+        """Whether the last render folded a lookahead trace (fs_options.lookahead)."""
+        f = C.c_int()
+        _check(gpu_lib().fs_last_render_lookahead(self.ctx, C.byref(f)), "fs_last_render_lookahead")
+        return bool(f.value)
 
     def counters(self):
         c = fs_counters()

@@ -1035,19 +1035,26 @@ void DisplayFrame::Reset() {
   samples_ = 0;
   if (frame_) fs_frame_reset(frame_);
 }
+// The planes are read into page-locked buffers the device frame owns
+// (fs_frame_map): the window loop's per-frame display read runs at pinned
+// PCIe speed and no copy into pageable memory follows (ABI 9). Without a
+// device frame (creation failed, LastTraceStatus says why) they are zeros.
 uint8* DisplayFrame::GetDisplayBuffer() {
-  display_.resize(3 * (size_t)width_ * height_);
-  if (frame_) fs_frame_read(frame_, FS_PLANE_DISPLAY, display_.data(), display_.size());
+  const void* p = nullptr;
+  if (frame_ && fs_frame_map(frame_, FS_PLANE_DISPLAY, &p) == FS_OK) return (uint8*)p;
+  display_.assign(3 * (size_t)width_ * height_, 0);
   return display_.data();
 }
 const float32* DisplayFrame::GetRenderTarget() {
-  color_.resize(3 * (size_t)width_ * height_);
-  if (frame_) fs_frame_read(frame_, FS_PLANE_COLOR, color_.data(), color_.size() * 4);
+  const void* p = nullptr;
+  if (frame_ && fs_frame_map(frame_, FS_PLANE_COLOR, &p) == FS_OK) return (const float32*)p;
+  color_.assign(3 * (size_t)width_ * height_, 0.0f);
   return color_.data();
 }
 const uint32* DisplayFrame::GetCountBuffer() {
-  count_.resize((size_t)width_ * height_);
-  if (frame_) fs_frame_read(frame_, FS_PLANE_COUNT, count_.data(), count_.size() * 4);
+  const void* p = nullptr;
+  if (frame_ && fs_frame_map(frame_, FS_PLANE_COUNT, &p) == FS_OK) return (const uint32*)p;
+  count_.assign((size_t)width_ * height_, 0u);
   return count_.data();
 }
 

@@ -354,7 +354,8 @@ class DisplayFrame {
   DisplayFrame(uint32 width, uint32 height);
   ~DisplayFrame();
   void Reset();
-  // Host copies are refreshed from the device on access.
+  // Host copies (page-locked, owned by the frame) are refreshed from the
+  // device on access; a pointer stays valid until the next access of that plane.
   uint8* GetDisplayBuffer();
   const float32* GetRenderTarget();
   const uint32* GetCountBuffer();

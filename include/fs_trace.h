@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FS_ABI_VERSION 8
+#define FS_ABI_VERSION 9
 #define FS_NORMAL_TABLE_SIZE 32768u /* material.cpp:17  InitializeMaterials */
 #define FS_MAX_TRACE_DEPTH 8u       /* engine.cpp:16   kMaximumTraceDepth */
 #define FS_NO_INDEX 0xFFFFFFFFu
@@ -273,6 +273,15 @@ typedef struct fs_options {
                                   one-group launch exceeds it renders in parts of its owned tiles
                                   and, below one tile per part, in launches of fewer samples per
                                   block: frames are identical (ABI 8) */
+  uint32_t lookahead;          /* 1 (default): a render of at most 4 spp over the whole frame
+                                  (tile_stride 1, no counters) also traces, in the background on
+                                  a stream of its own, the samples the next call would add
+                                  (sample_base + spp); the next fs_render with the same camera,
+                                  scene, options and parameters but that sample_base folds those
+                                  path records instead of tracing, and any other render discards
+                                  them. The reference's window loop (one TraceScene per displayed
+                                  frame, main.cpp:157-163) then keeps the GPU busy while the host
+                                  reads the frame. Frames are identical; 0 off (ABI 9) */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */
@@ -309,13 +318,19 @@ int fs_frame_destroy(fs_frame* frame);
 int fs_frame_reset(fs_frame* frame);              /* DisplayFrame::Reset */
 /* Copies one plane (all pixels) to host memory of the plane's byte size. */
 int fs_frame_read(fs_frame* frame, int plane, void* host_dst, size_t bytes);
+/* Copies one plane to a page-locked host buffer the frame owns and sets
+ * *host to it: valid until the next fs_frame_map of that plane or
+ * fs_frame_destroy. DisplayFrame::GetDisplayBuffer (frame.h) returns it
+ * (ABI 9: PCIe at pinned speed, no copy into pageable memory). */
+int fs_frame_map(fs_frame* frame, int plane, const void** host);
 /* Overwrites one plane from host memory (resume / test setup). */
 int fs_frame_write(fs_frame* frame, int plane, const void* host_src,
                    size_t bytes);
 
 /* ---- the hot path ------------------------------------------------------ */
 /* Adds params->spp samples per owned pixel into frame; asynchronous on the
- * context stream; fs_synchronize() waits. counters may be NULL. */
+ * context stream; fs_synchronize() waits (for the frame; a background
+ * lookahead trace, fs_options.lookahead, runs on). counters may be NULL. */
 int fs_render(fs_context* ctx, const fs_camera* camera,
               const fs_render_params* params, fs_frame* frame);
 int fs_synchronize(fs_context* ctx);
@@ -357,6 +372,9 @@ const char* fs_last_kernel(fs_context* ctx);
  * the samples per pixel of the largest one (renders are cut into launches of
  * sample groups). Profiling aid, no reference counterpart. */
 int fs_last_render_launches(fs_context* ctx, uint32_t* launches, uint32_t* spp_per_launch);
+/* 1 when the last fs_render folded a lookahead trace (fs_options.lookahead)
+ * instead of tracing, else 0 (ABI 9). Test and profiling aid. */
+int fs_last_render_lookahead(fs_context* ctx, int* folded);
 
 /* ---- multi-GPU (RCCL over xGMI) ---------------------------------------- */
 #define FS_COMM_ID_BYTES 128

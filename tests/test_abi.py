@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_abi_version_and_errors_without_device():
     lib = fsamd.gpu_lib()
-    assert lib.fs_abi_version() == 8
+    assert lib.fs_abi_version() == 9
     assert lib.fs_upload_scene(None, None) == -1  # FS_ERR_INVALID
     assert b"null" in lib.fs_last_error()
     assert lib.fs_render(None, None, None, None) == -1
@@ -49,7 +49,7 @@ def test_options_defaults_and_validation_without_device():
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
                  "small_mesh_tris": 16, "park_lanes_small": 6,
-                 "lds_rows": 1, "record_budget_mb": 0}
+                 "lds_rows": 1, "record_budget_mb": 0, "lookahead": 1}
     assert fsamd.parse_variant("schedule=parked@park_lanes=8") == {"schedule": "parked", "park_lanes": 8}
     assert fsamd.options(schedule="parked").schedule == 2
     lib = fsamd.gpu_lib()
@@ -57,7 +57,8 @@ def test_options_defaults_and_validation_without_device():
     assert lib.fs_set_options(None, C.byref(o)) == -1
     d, n = C.c_uint64(), C.c_uint64()
     for bad in ({"bvh_leaf": 0}, {"bvh_leaf": 16}, {"bvh_bins": 65}, {"samples_per_block": 65}, {"schedule": 3}, {"xcd_bands": 3},
-                {"persist": 2}, {"small_mesh_tris": 65}, {"park_lanes": 65}, {"lds_rows": 2}):
+                {"persist": 2}, {"small_mesh_tris": 65}, {"park_lanes": 65}, {"lds_rows": 2},
+                {"lookahead": 2}):
         ob = fsamd.options(**bad)
         assert lib.fs_prepare_digest(C.c_void_p(1), C.byref(ob), C.byref(d), C.byref(n), None) == -1, bad
     with pytest.raises(fsamd.FsError):
@@ -107,6 +108,45 @@ def test_launch_plan_small_budget_without_device():
     assert p.parts == 1 and p.samples_per_block == 16
     with pytest.raises(fsamd.FsError, match="below one tile"):
         _plan(256, 200, 20, 100000, 88)
+
+
+def test_launch_plan_of_fewer_samples_than_a_block_without_device():
+    """a 1-spp launch (the drop-in loop's TraceScene) sizes its
+    path records to the samples it holds, not to samples_per_block (16)."""
+    p = _plan(1920, 1080, 1)
+    assert (p.parts, p.samples_per_block, p.groups_per_launch, p.launches) == (1, 1, 1, 1)
+    assert p.record_bytes_per_launch == 510 * 64 * 64 * 1 * 88
+    p = _plan(1920, 1080, 3)
+    assert (p.samples_per_block, p.launches) == (3, 1)
+    assert _plan(1920, 1080, 40).samples_per_block == 16
+
+
+def test_deep_mesh_bvh_fits_the_walk_stack_without_device():
+    """the node step writes the walk stack at sp on every trip,
+    in bounds because the host builder stops splitting at depth
+    kTraversalStack - 1 = 23. A mesh of 200 triangles on a geometric
+    progression (every SAH split peels off one face) would build a tree of
+    depth ~200 without the guard."""
+    import json
+
+    import descbuild
+
+    b = descbuild.DescBuilder()
+    m = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.5, 0.5, 0.5))
+    pos, faces = [], []
+    for i in range(200):
+        x = 1.5 ** i
+        pos += [[x, 0, 0], [x * 1.01, 1, 0], [x * 1.02, 0, 1]]
+        faces.append([3 * i, 3 * i + 1, 3 * i + 2])
+    b.mesh(m, pos, faces)
+    desc = b.build()
+    buf = C.create_string_buffer(1 << 16)
+    lib = fsamd.gpu_lib()
+    o = fsamd.options()
+    assert lib.fs_bvh_quality(desc, C.byref(o), buf, len(buf)) == 0, lib.fs_last_error()
+    q = json.loads(buf.value.decode())
+    assert len(q) == 1 and q[0]["faces"] == 200
+    assert 15 < q[0]["depth"] <= 23  # deep, and within the 24-entry stack
 
 
 def test_create_fails_cleanly_without_a_gpu():

@@ -5,8 +5,9 @@ hand-picked geometry; these draw the geometry: spheres, planes, discs, both
 quad kinds and rotated cuboids at random places and sizes, small meshes of
 random faces (tested face by face), and a cloud of random triangles large
 enough for a BVH walk (with parking forced on one schedule), in the Cornell
-room, with every material whose path needs no device transcendental (no
-frost, no thin lens). Objects overlap, intersect and nest at random, so
+room, with every material; with transcendental=True also frosted glass,
+sphere-mapped textured spheres, a textured sky and a thin-lens camera (the
+fs_libm.h sinf/cosf/atan2f paths). Objects overlap, intersect and nest at random, so
 segments start inside boxes, graze faces and tie more often than in the bench
 scenes."""
 import numpy as np
@@ -19,7 +20,7 @@ from test_gpu_parity import assert_parity, gpu_render, oracle_render
 pytestmark = pytest.mark.gpu
 
 
-def random_scene(seed, cloud_tris=3000, crowd=0, textured=False):
+def random_scene(seed, cloud_tris=3000, crowd=0, textured=False, transcendental=False):
     rng = np.random.default_rng(seed)
     b = DescBuilder()
     white = b.material(fsamd.MAT_DIFFUSE, diffuse=(0.73, 0.73, 0.73))
@@ -38,6 +39,9 @@ def random_scene(seed, cloud_tris=3000, crowd=0, textured=False):
         b.material(fsamd.MAT_FOG, diffuse=col(), density=u(0.001, 0.05)),
         b.material(fsamd.MAT_LIGHT, emissive=tuple(3 * x for x in col())),
     ]
+    if transcendental:  # frosted glass: the refraction rotated by cosf/sinf of a drawn angle
+        mats += [b.material(fsamd.MAT_GLASS, diffuse=col(), index=u(0.5, 1.6), reflectivity=u(0.0, 0.5),
+                            frost=u(0.02, 1.0)) for _ in range(2)]
     pick = lambda: mats[int(rng.integers(len(mats)))]  # noqa: E731
     flat = pick  # materials of objects whose texture lookup is bit-exact (planar maps, mesh texcoords)
     if textured:  # diffuse maps of random sizes and scales; spheres (atan2f maps) never take them
@@ -45,11 +49,17 @@ def random_scene(seed, cloud_tris=3000, crowd=0, textured=False):
                for _ in range(2)]
         tmats = [b.material(fsamd.MAT_DIFFUSE, diffuse=col(), texture=t, texture_scale=u(0.05, 3.0)) for t in tex]
         flat = lambda: tmats[int(rng.integers(2))] if rng.random() < 0.6 else pick()  # noqa: E731
+    if textured and transcendental:  # spheres take maps too (atan2f), and the sky
+        sphere_pick = lambda: tmats[int(rng.integers(2))] if rng.random() < 0.6 else pick()  # noqa: E731
+        b.sky = b.material(fsamd.MAT_LIGHT, emissive=tuple(0.3 * x for x in col()), texture=tex[0],
+                           texture_scale=1.0)
+    else:
+        sphere_pick = pick
     cornell_room(b, white, red, light)
     p = lambda: [u(-8, 8), u(1, 18), u(-8, 8)]  # noqa: E731
     n = lambda: list(rng.normal(size=3))  # noqa: E731
     for _ in range(int(rng.integers(2, 5))):
-        b.obj(fsamd.OBJ_SPHERE, pick(), p() + [u(0.5, 3)])
+        b.obj(fsamd.OBJ_SPHERE, sphere_pick(), p() + [u(0.5, 3)])
     if rng.random() < 0.5:
         nv = np.array(n())
         nv /= np.linalg.norm(nv)
@@ -158,4 +168,20 @@ def test_random_scene_larger_frame_bit_exact(seed, gpu_renderer):
     cam = CAMS[seed % 2]
     out = gpu_render(gpu_renderer, ptr, cam, 256, 192, 16)
     ref = oracle_render(ptr, cam, 256, 192, 16)
+    assert_parity(out, ref, exact=True)
+
+
+@pytest.mark.parametrize("seed,textured", [(600, False), (601, True), (602, False), (603, True), (604, True),
+                                           (605, False)])
+def test_random_scene_with_transcendentals_bit_exact(seed, textured, gpu_renderer):
+    """Frosted glass, sphere-mapped spheres, a textured sky and a thin-lens
+    camera of random aperture and focal depth: the
+    device's sinf/cosf/atan2f are the host C library's bits (fs_libm.h)."""
+    rng = np.random.default_rng(seed)
+    b = random_scene(seed, cloud_tris=1500, textured=textured, transcendental=True)
+    ptr = b.build()
+    cam = fsamd.camera((float(rng.uniform(-3, 3)), 10, -34), (0, float(rng.uniform(6, 12)), 0), fov_y=45,
+                       aperture=float(rng.uniform(0.1, 2.0)), focal_depth=float(rng.uniform(20, 45)))
+    out = gpu_render(gpu_renderer, ptr, cam, 80, 60, 8)
+    ref = oracle_render(ptr, cam, 80, 60, 8)
     assert_parity(out, ref, exact=True)

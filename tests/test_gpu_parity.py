@@ -5,9 +5,12 @@ per-(pixel,sample) seeds:
   * per channel |gpu - ref| <= 1e-3 + 1e-2*|ref| for >= 99.9% of channels,
   * RGB8 display identical for >= 99.5% of pixels,
   * image-mean relative error <= 1e-4.
-Scenes whose path uses no transcendental on the device (no thin lens, no
-frosted glass) are required to be bit-exact: the kernel keeps the reference's
-float operation order and compiles with -ffp-contract=off.
+Every scene is required to be bit-exact: the kernel keeps the reference's
+float operation order and compiles with -ffp-contract=off, and the float
+sinf/cosf/atan2f of the thin lens, frosted glass and sphere maps are
+restatements of the host C library's (csrc/fs_libm.h, checked against it bit
+for bit in tests/test_exact_rewrites.py). The tolerance is kept for the
+bench-scale comparisons against the reference's octree.
 """
 import os
 
@@ -194,21 +197,27 @@ def test_face_ties_and_slivers_bit_exact(small_mesh_tris, gpu_renderer):
     assert_parity(out, ref, exact=True)
 
 
-def test_frosted_glass_within_tolerance(gpu_renderer):
-    # frost > 0 rotates by cos/sin (vector3.h:315): ocml vs glibc may differ by an ulp
+def test_frosted_glass_bit_exact(gpu_renderer):
+    # frost > 0 rotates by cos/sin of the drawn angle (vector3.h:315-333):
+    # fs_libm.h gives the host libm's bits
     b = zoo(frost=0.2)
     ptr = b.build()
     out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
+    assert gpu_renderer.last_kernel()[:-1].split(", ")[7] == "true"  # the TRIG instantiation
     ref = oracle_render(ptr, CAM, 96, 72, 16)
-    assert_parity(out, ref, exact=False)
+    assert_parity(out, ref, exact=True)
 
 
-def test_thin_lens_camera_within_tolerance(scene_dir, gpu_renderer):
+@pytest.mark.parametrize("aperture,focal", [(1.5, 36.0), (0.4, 20.0)])
+def test_thin_lens_camera_bit_exact(aperture, focal, scene_dir, gpu_renderer):
+    # the lens offset's cosf/sinf of the drawn angle (engine.cpp:221-244);
+    # the reference's default camera has the lens on (camera.cpp:6-24)
     s = load_scene("c2", scene_dir)
-    cam = fsamd.camera((0, 10, -34), (0, 10, 0), fov_y=40, aperture=1.5, focal_depth=36)
+    cam = fsamd.camera((0, 10, -34), (0, 10, 0), fov_y=40, aperture=aperture, focal_depth=focal)
     out = gpu_render(gpu_renderer, s, cam, 80, 60, 16)
+    assert gpu_renderer.last_kernel()[:-1].split(", ")[7] == "true"  # the TRIG instantiation
     ref = oracle_render(s.desc_ptr(), cam, 80, 60, 16)
-    assert_parity(out, ref, exact=False)
+    assert_parity(out, ref, exact=True)
 
 
 def test_fast_render_and_default_camera(scene_dir, gpu_renderer):
@@ -278,7 +287,7 @@ def textured_scene(spheres):
     meshes with texcoords; a texcoord-less mesh after a planar writer (the
     reference keeps the earlier surface_texcoords); negative and scaled
     coordinates; non-power-of-two maps. With spheres=True also sphere-mapped
-    spheres and a textured Light sky (atan2f: tolerance)."""
+    spheres and a textured Light sky (atan2f, fs_libm.h)."""
     rng = np.random.default_rng(7)
     b = DescBuilder()
     t0 = b.texture(rng.random((23, 37, 3)))
@@ -332,13 +341,13 @@ def test_textures_planar_and_mesh_bit_exact(gpu_renderer):
     assert not np.array_equal(plain[fsamd.PLANE_COLOR], out[fsamd.PLANE_COLOR])
 
 
-def test_textures_sphere_map_and_sky_within_tolerance(gpu_renderer):
-    # sphere_map_texcoords calls atan2f (ocml here, the C runtime in the reference)
+def test_textures_sphere_map_and_sky_bit_exact(gpu_renderer):
+    # sphere_map_texcoords calls atan2f (intersect.cpp:769-784): fs_libm.h
     b = textured_scene(spheres=True)
     ptr = b.build()
     out = gpu_render(gpu_renderer, ptr, CAM, 96, 72, 16)
     ref = oracle_render(ptr, CAM, 96, 72, 16)
-    assert_parity(out, ref, exact=False)
+    assert_parity(out, ref, exact=True)
 
 
 def test_textured_scene_rejects_parked_schedule(gpu_renderer):

@@ -25,17 +25,23 @@ LIMITS = {
     # cuboid cull took the segment's slopes instead of three v_rcp of its own
     # that the compiler hoisted out of the object loop and spilled (C4 +4 %,
     # C2 +5 %, write-backs 176 -> 95 B per sample, profiles/r05/ab_spills.log)
-    "render_kernel_lean<false, 6, false, true, false, false, false>": (24, 14, 80),
+    "render_kernel_lean<false, 6, false, true, false, false, false, false>": (24, 14, 80),
     # LEAN schedule: scenes with BVH walks and no large mesh (no bench config
     # runs it). 24 -> 12 B/lane with the cuboid cull on the segment's slopes,
     # 20 with the zero-length shortcut (its division behind a branch)
-    "render_kernel_lean<false, 6, false, false, false, false, false>": (24, 14, 80),
+    "render_kernel_lean<false, 6, false, false, false, false, false, false>": (24, 14, 80),
     # LEAN without walks (NOWALK: every mesh small, no walk stack, 8 waves per
     # SIMD): C1 and C2. 44 -> 40 B/lane without the backward pass (C2 +8.5 %);
     # 40 -> 48 with the round-5 face loop and no SLP vectorization (C2 +8.9 %,
     # profiles/r05/ab_noslp.log); 48 -> 24 with the cuboid cull on the
     # segment's slopes (profiles/r05/ab_spills.log)
-    "render_kernel_lean<false, 8, false, false, false, false, true>": (24, 16, 64),
+    "render_kernel_lean<false, 8, false, false, false, false, true, false>": (24, 16, 64),
+    # The TRIG twins (round 6: a thin-lens camera or frosted glass; the host
+    # libm's sinf/cosf restated in double, csrc/fs_libm.h): the parked-walk
+    # kernel reserves 28 B/lane, its one spilled value reloaded only on Fog paths
+    "render_kernel_lean<false, 6, false, true, false, false, false, true>": (28, 14, 80),
+    "render_kernel_lean<false, 6, false, false, false, false, false, true>": (24, 14, 80),
+    "render_kernel_lean<false, 8, false, false, false, false, true, true>": (24, 16, 64),
 }
 
 

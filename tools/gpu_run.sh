@@ -7,10 +7,12 @@
 #   smoke                        __graft_entry__.smoke()
 #   bench:SCENE[:WxH[:STEPS]]    one bench.py line -> bench_SCENE_WxH.json (C4 1080p adds the CPU baseline)
 #   prof[:SCENE]                 rocprofv3 --kernel-trace --stats of the bench command -> prof_SCENE/
-#   pmc:SCENE:WxH:SPP            PMC passes (one counter group each) + tools/pmc_summary.py
+#   sweep[:SCENES]               tools/spp_sweep.py: one launch's trace time against its samples
+#   pmc:SCENE:WxH:SPP[:STEPS]    PMC passes (one counter group each) + tools/pmc_summary.py
 #                                -> pmc_SCENE_WxH.json, stamped with the code object's digest
 #   ab:VARIANTS:SCENES:SPP:ROUNDS   tools/perf_ab.py (fs_options A/B in one process)
 #   libab:LIBS:SCENES:SPP:ROUNDS    alternating processes over in-tree builds (space-separated .so names)
+#   wt[:SCENES[:SPPS]]           per-wave end/drain times of the trace kernel (needs libfsgpu_wt.so)
 #   phase:SCENES:SPP             per-phase cycle split (needs the in-tree libfsgpu_prof.so)
 #   lib:NAME                     the steps after it load final-stage-path-tracer-2-0_amd/NAME (an A/B build)
 #                                through FSAMD_GPU_LIB; "lib:" alone returns to the product libfsgpu.so
@@ -55,10 +57,10 @@ for step in "$@"; do
         || fail "$step" $? $OUT/prof_$sc.err
       find $OUT/prof_$sc -name "*kernel_stats.csv" -exec cut -c1-160 {} \; ;;
     pmc)
-      sc=$a1; wh=$a2; w=${wh%x*}; h=${wh#*x}; spp=$a3
-      d=$OUT/pmc_${sc}_${wh}
+      sc=$a1; wh=$a2; w=${wh%x*}; h=${wh#*x}; spp=$a3; pst=${a4:-1}; pwu=0; [ "$pst" -gt 1 ] && pwu=2
+      d=$OUT/pmc_${sc}_${wh}$([ "$spp" -lt 64 ] && echo "_$spp")
       mkdir -p $d
-      cmd="python3 bench.py --scene $sc --steps 1 --warmup 0 --spp $spp --no-cpu --width $w --height $h"
+      cmd="python3 bench.py --scene $sc --steps $pst --warmup $pwu --spp $spp --no-cpu --width $w --height $h"
       i=0
       for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH" \
                  "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM" \
@@ -73,9 +75,12 @@ for step in "$@"; do
       # counters are averaged per dispatch: normalise by the samples of one launch (the render may take several)
       lspp=$(python3 -c "import json; print([json.loads(l) for l in open('$d/p1.out') if l.startswith('{')][-1]['roofline']['spp_per_launch'])") \
         || fail "$step" $?
-      python3 tools/pmc_summary.py $d "$kern" $OUT/pmc_${sc}_${wh}.json "$sc ${wh} x $spp spp in launches of $lspp spp" \
+      python3 tools/pmc_summary.py $d "$kern" $d.json "$sc ${wh} x $spp spp in launches of $lspp spp" \
         $((w * h * lspp)) > $d/summary.log 2>&1 || fail "$step" $? $d/summary.log
-      grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $OUT/pmc_${sc}_${wh}.json ;;
+      grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $d.json ;;
+    sweep)
+      timeout -k 10 600 python3 tools/spp_sweep.py ${a1:-c4,c2} > $OUT/spp_sweep.log 2>&1 || fail "$step" $? $OUT/spp_sweep.log
+      cat $OUT/spp_sweep.log ;;
     ab)
       log=$OUT/ab_$(date +%H%M%S).log
       timeout -k 10 900 python tools/perf_ab.py "$a1" "$a2" ${a3:-256} ${a4:-2} > $log 2>&1 || fail "$step" $? $log
@@ -90,6 +95,24 @@ for step in "$@"; do
         done
       done
       grep -E "^==|variant|md5" $log ;;
+    dropin)
+      # the reference's window loop through the C++ mirror (examples/dropin_rate), then the same
+      # loop under a kernel + memory-copy trace (per-frame split: trace, fold, copies, gaps)
+      sc=${a1:-c4}; n=${a2:-256}
+      p=$(python3 -c "import sys; sys.path.insert(0, 'final-stage-path-tracer-2-0_amd'); import scenes; print(scenes.write('$sc', '$OUT/scenes/$sc'))") \
+        || fail "$step" $?
+      timeout -k 10 300 ./examples/dropin_rate $p 1920 1080 $n > $OUT/dropin_${sc}_1920x1080.json \
+        2> $OUT/dropin_$sc.err || fail "$step" $? $OUT/dropin_$sc.err
+      cat $OUT/dropin_${sc}_1920x1080.json
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+        -d $OUT/dropin_prof_$sc -o trace -- ./examples/dropin_rate $p 1920 1080 64 > $OUT/dropin_prof_$sc.json \
+        2> $OUT/dropin_prof_$sc.err || fail "$step" $? $OUT/dropin_prof_$sc.err
+      python3 tools/dropin_split.py $OUT/dropin_prof_$sc > $OUT/dropin_split_$sc.log 2>&1 || fail "$step" $? $OUT/dropin_split_$sc.log
+      cat $OUT/dropin_split_$sc.log ;;
+    wt)
+      FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/libfsgpu_wt.so timeout -k 10 600 \
+        python tools/wave_times.py ${a1:-c4,c2} ${a2:-1,2,16} > $OUT/wave_times.log 2>&1 || fail "$step" $? $OUT/wave_times.log
+      grep -E "==|waves" $OUT/wave_times.log ;;
     phase)
       FSAMD_GPU_LIB=$PWD/final-stage-path-tracer-2-0_amd/libfsgpu_prof.so timeout -k 10 600 \
         python tools/phase_prof.py "$a1" ${a2:-64} > $OUT/phase.log 2>&1 || fail "$step" $? $OUT/phase.log
