@@ -71,8 +71,10 @@ S_NODE, S_TRI, S_OBJ, S_SEG, S_SAMPLE = 64, 64, 128, 96, 24
 CPU_CALIBRATION = ("oracle vs reference on SURVEY's probe scenes (8 threads, build container, DESIGN §6, "
                    "profiles/r04/cpu_calibration.log): 250k probe rate x1.22 at 3.52 vs 5.02 segments/sample and "
                    "153 vs 137 triangle tests per segment, i.e. x0.96 per triangle test; 1M probe x1.11 at 3.50 vs "
-                   "5.05 and 508 vs 451, x0.87 per triangle test; the reference cannot be built here for a "
-                   "same-machine run")
+                   "5.05 and 508 vs 451, x0.87 per triangle test; C1's 10.8 vs 15.8 triangle tests per segment is "
+                   "mesh grouping: the same geometry with the room's walls and light as one 12-face mesh (one "
+                   "Cornell OBJ) gives 16.0 (tools/c1_grouping.py, profiles/r06/c1_grouping.log); the reference "
+                   "cannot be built here for a same-machine run")
 
 
 def parse():
