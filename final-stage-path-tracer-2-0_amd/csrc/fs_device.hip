@@ -2589,7 +2589,10 @@ int check_params(const fs_render_params* p, const fs_frame* f, uint32_t* ts, uin
 // kernels (6), the parked-walk kernel (6; 5 waves with 96 VGPRs measured
 // C4 -6.5 %, 7 waves with a 22-entry stack -9.5 %) and the NOWALK kernel (8:
 // no LDS stack, its LDS rows take 4 KiB per wave; 6 waves -4 %, 7 -1.5 %).
-constexpr int kLeanWaves = 6, kSuspWaves = 6, kNowalkWaves = 8;
+#ifndef FS_SUSP_WAVES
+#define FS_SUSP_WAVES 6  // A/B builds only (make ab DEFS=-DFS_SUSP_WAVES=7)
+#endif
+constexpr int kLeanWaves = 6, kSuspWaves = FS_SUSP_WAVES, kNowalkWaves = 8;
 
 #define FS_STR2(x) #x
 #define FS_STR(x) FS_STR2(x)
@@ -3357,7 +3360,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     }
     const size_t need = rows_bytes(grid * kBlock, pb * params->spp * kBlock, tex_rec, mm);
     if (A.rows[s].bytes < need || A.aov[s].bytes < 24 * px || !A.queues[s].p) {
-      FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace still uses the old buffers
+      FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace and fold still use the old buffers
+      FS_HIP(hipStreamSynchronize(ctx->stream));
       ready = !ensure(&A.rows[s], need) && !ensure(&A.aov[s], 24 * px) &&
               !ensure(&A.queues[s], 8 * dev::kQueueStride * sizeof(uint32_t));
       if (!ready) (void)hipGetLastError();  // no room: this call has no lookahead

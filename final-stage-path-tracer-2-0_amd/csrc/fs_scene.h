@@ -67,7 +67,10 @@ FS_HD uint32_t leaf_word(uint32_t count, uint32_t first) {
   return kLeafBit | (count << kLeafCountShift) | first;
 }
 FS_HD uint32_t leaf_count(uint32_t w) { return (w >> kLeafCountShift) & 0xFu; }
-constexpr uint32_t kTraversalStack = 24;  // BVH depth bound (builder enforces); the LDS stack bounds the waves per CU
+#ifndef FS_TRAVERSAL_STACK
+#define FS_TRAVERSAL_STACK 24  // A/B builds only (make ab DEFS=-DFS_TRAVERSAL_STACK=22)
+#endif
+constexpr uint32_t kTraversalStack = FS_TRAVERSAL_STACK;  // BVH depth bound (builder enforces); the LDS stack bounds the waves per CU
 constexpr uint32_t kMaxSmallMeshTris = 64;  // fs_options.small_mesh_tris bound
 
 // Triangle record: the operands of the reference test (intersect.cpp:357-419)

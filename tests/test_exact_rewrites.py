@@ -172,3 +172,4 @@ def test_libm_atan2_matches_host(tmp_path_factory):
     assert bad == 0 and checked > 6e8, out
     checked, bad, out = _run(exe, "atan2", 20_000_000, 5)
     assert bad == 0 and checked >= 4e7, out
+

@@ -10,6 +10,7 @@ build and one with FS_UPLOAD_GPU_BVH; their renders alternate and every frame
 is compared with the first (the trees differ, the frames must not).
 """
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -26,7 +27,7 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     variants = (sys.argv[4] if len(sys.argv) > 4 else "host,device").split(",")
     W, H = 1920, 1080
-    tmp = os.path.join(ROOT, "gpurun_out", "scenes")
+    tmp = os.path.join(tempfile.gettempdir(), "fs_scenes")
     for name in names:
         p = scenes.write(name, os.path.join(tmp, name))
         fsamd.reset_main_rng()

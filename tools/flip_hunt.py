@@ -9,6 +9,7 @@ mismatching (x, y, k) with both colours, normals and depths as JSON.
 """
 import json
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -24,7 +25,7 @@ def main():
     name, W, H, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     out_path = sys.argv[5] if len(sys.argv) > 5 else os.path.join(ROOT, "gpurun_out", f"flips_{name}.json")
     variant = fsamd.parse_variant(sys.argv[6]) if len(sys.argv) > 6 else {}
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

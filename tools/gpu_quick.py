@@ -1,6 +1,7 @@
 """Quick GPU check: GPU vs oracle on small renders + 1080p timing per scene.
 usage: python tools/gpu_quick.py c1:64x64x16 c4:128x72x4 ... [--time c2,c4]"""
 import os
+import tempfile
 import sys
 import time
 
@@ -13,7 +14,7 @@ import fsamd  # noqa: E402
 import oracle_py  # noqa: E402
 import scenes  # noqa: E402
 
-TMP = os.path.join(ROOT, "gpurun_out", "scenes")
+TMP = os.path.join(tempfile.gettempdir(), "fs_scenes")
 _cache = {}
 
 

@@ -99,7 +99,7 @@ for step in "$@"; do
       # the reference's window loop through the C++ mirror (examples/dropin_rate), then the same
       # loop under a kernel + memory-copy trace (per-frame split: trace, fold, copies, gaps)
       sc=${a1:-c4}; n=${a2:-256}
-      p=$(python3 -c "import sys; sys.path.insert(0, 'final-stage-path-tracer-2-0_amd'); import scenes; print(scenes.write('$sc', '$OUT/scenes/$sc'))") \
+      p=$(python3 -c "import sys; sys.path.insert(0, 'final-stage-path-tracer-2-0_amd'); import scenes; print(scenes.write('$sc', '/tmp/fs_scenes/$sc'))") \
         || fail "$step" $?
       timeout -k 10 300 ./examples/dropin_rate $p 1920 1080 $n > $OUT/dropin_${sc}_1920x1080.json \
         2> $OUT/dropin_$sc.err || fail "$step" $? $OUT/dropin_$sc.err

@@ -1,6 +1,7 @@
 """A/B of BVH build settings in one process: rebuild + time.
 usage: python tools/leaf_ab.py VALUES scenes [spp] [FIELD]   (fs_options field, default bvh_leaf; e.g. bvh_bins)"""
 import os
+import tempfile
 import sys
 import time
 
@@ -17,7 +18,7 @@ spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 env = sys.argv[4] if len(sys.argv) > 4 else "bvh_leaf"
 W, H = 1920, 1080
 for name in names:
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

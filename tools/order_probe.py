@@ -5,6 +5,7 @@ runs with the floor's or walls' hit as its t limit. The reordered scene is a
 different scene for ties and the mesh-root cull, so only the times compare.
 usage: python tools/order_probe.py [spp] [rounds]"""
 import os
+import tempfile
 import re
 import sys
 
@@ -17,7 +18,7 @@ import scenes  # noqa: E402
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 W, H = 1920, 1080
-d = os.path.join(ROOT, "gpurun_out", "scenes", "c3_order")
+d = os.path.join(tempfile.gettempdir(), "fs_scenes", "c3_order")
 p = scenes.write("c3", d)
 text = open(p).read()
 blocks = re.findall(r"mesh\n\{\n  file atrium_(\w+)\.obj\n  material \w+\n\}\n", text)

@@ -2,6 +2,7 @@
 usage: python tools/perf_ab.py variants scenes [spp] [rounds]
 (a variant is default or fields joined by @, e.g. "schedule=parked@xcd_bands=1@park_lanes=8")"""
 import os
+import tempfile
 import sys
 import time
 
@@ -23,7 +24,7 @@ def main():
     spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
     rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 3
     W, H = 1920, 1080
-    tmp = os.path.join(ROOT, "gpurun_out", "scenes")
+    tmp = os.path.join(tempfile.gettempdir(), "fs_scenes")
     for name in names:
         p = scenes.write(name, os.path.join(tmp, name))
         fsamd.reset_main_rng()

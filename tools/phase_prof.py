@@ -2,6 +2,7 @@
 make -C final-stage-path-tracer-2-0_amd libfsgpu_prof.so).
 usage: python tools/phase_prof.py scenes [spp]"""
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,7 +16,7 @@ names = sys.argv[1].split(",")
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 W, H = 1920, 1080
 for name in names:
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

@@ -4,6 +4,7 @@ the slowest rank's render time per N (gather excluded).
 usage: python tools/scaling_sim.py [scene] [spp] [Ns] [variants]
 (variants: comma list of fs_options settings, e.g. "groups=1,default"; TS=<n> sets the tile size)"""
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,7 +19,7 @@ def main():
     ns = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "1,2,4,8").split(",")]
     variants = (sys.argv[4] if len(sys.argv) > 4 else "default").split(",")
     W, H = 1920, 1080
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

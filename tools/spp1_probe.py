@@ -1,13 +1,14 @@
 """One-sample-per-pixel launches (the reference's TraceScene-per-frame loop)
 under a few fs_options, with and without the display-byte readback
 (measurement aid). usage: python tools/spp1_probe.py"""
-import os, sys, time
+import os
+import tempfile, sys, time
 ROOT = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
 sys.path.insert(0, os.path.join(ROOT, "final-stage-path-tracer-2-0_amd"))
 import numpy as np, fsamd, scenes
 W, H = 1920, 1080
 for name in ["c4", "c2"]:
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

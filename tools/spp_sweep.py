@@ -5,6 +5,7 @@ of samples_per_block 1, the median HIP-event time of the trace kernel. A
 fixed per-launch cost shows as the intercept of ms against k.
 usage: python tools/spp_sweep.py [scenes] [W] [H]"""
 import os
+import tempfile
 import statistics
 import sys
 
@@ -17,7 +18,7 @@ names = (sys.argv[1] if len(sys.argv) > 1 else "c4,c2").split(",")
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 1920
 H = int(sys.argv[3]) if len(sys.argv) > 3 else 1080
 for name in names:
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

@@ -1,6 +1,7 @@
 """Render time against the tile size (the unit of XCD placement and of the
 multi-GPU partition; measurement aid). usage: python tools/tile_probe.py [spp] [rounds]"""
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,7 +14,7 @@ spp = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 W, H = 1920, 1080
 for name in ("c4", "c3", "c2"):
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()

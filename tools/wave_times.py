@@ -4,6 +4,7 @@ time each wave ends and first finds every block queue empty, and how long
 waves run on after that (measurement aid for the 1-spp drop-in launch, VERDICT
 r5 item 3). usage: python tools/wave_times.py [scenes] [spp,...]"""
 import os
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,7 +18,7 @@ names = (sys.argv[1] if len(sys.argv) > 1 else "c4,c2").split(",")
 spps = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2,16").split(",")]
 W, H = 1920, 1080
 for name in names:
-    p = scenes.write(name, os.path.join(ROOT, "gpurun_out", "scenes", name))
+    p = scenes.write(name, os.path.join(tempfile.gettempdir(), "fs_scenes", name))
     fsamd.reset_main_rng()
     s = fsamd.HostScene.load(p)
     fsamd.initialize_materials()
