@@ -5,7 +5,7 @@
 // PCIe read of W x H x 3 bytes; TraceSceneBatch submits many samples at once.
 // Scene load and BVH build are excluded (one warm-up frame first).
 //
-//   dropin_rate <file.scene> <width> <height> <frames>
+//   dropin_rate <file.scene> <width> <height> <frames> [lookahead depth, default the library's]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +30,14 @@ int main(int argc, char** argv) {
   if (W < 2 || H < 2 || frames == 0) {
     std::fprintf(stderr, "width and height must be >= 2 and frames > 0\n");
     return 2;
+  }
+  if (argc > 5) {  // fs_options.lookahead: how many TraceScene calls ahead the device traces
+    base::TraceSettings ts = base::GetTraceSettings();
+    ts.options.lookahead = (uint32_t)std::atoi(argv[5]);
+    if (!base::SetTraceSettings(ts)) {
+      std::fprintf(stderr, "SetTraceSettings: %s\n", base::LastTraceError());
+      return 2;
+    }
   }
   base::DisplayFrame frame(W, H);
   base::TraceScene(camera, &scene, &frame);  // upload + BVH build, not timed
@@ -60,8 +68,9 @@ int main(int argc, char** argv) {
     return 1;
   }
   const double samples = (double)W * H * frames;
-  std::printf("{\"width\": %u, \"height\": %u, \"frames\": %u, \"loop_msamples_per_s\": %.2f, "
+  std::printf("{\"width\": %u, \"height\": %u, \"frames\": %u, \"lookahead\": %u, \"loop_msamples_per_s\": %.2f, "
               "\"loop_ms_per_frame\": %.3f, \"batch_msamples_per_s\": %.2f}\n",
-              W, H, frames, samples / loop_s / 1e6, loop_s * 1e3 / frames, samples / batch_s / 1e6);
+              W, H, frames, base::GetTraceSettings().options.lookahead, samples / loop_s / 1e6, loop_s * 1e3 / frames,
+              samples / batch_s / 1e6);
   return 0;
 }

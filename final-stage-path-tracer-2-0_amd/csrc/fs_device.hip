@@ -1647,7 +1647,7 @@ __device__ __forceinline__ TaskBlock decode_block(const Launch& P, const DevFram
   B.x0 = tx * P.tile_size + (micro % micro_per_side) * 8;
   B.y0 = ty * P.tile_size + (micro / micro_per_side) * 8;
   B.sample0 = P.sample_base + group * P.spp;
-  B.aov = group + 1 == P.groups;
+  B.aov = group + 1 == P.groups || P.aov_rows != 0;
   B.next = 0;
   if (B.x0 < F.width && B.y0 < F.height) {  // only in-frame pixels are enumerated
     B.vx = min(8u, F.width - B.x0);
@@ -1878,12 +1878,14 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         }
         if (depth == 0 && aov) {  // the last sample's AOVs remain
           const DevFrame& Fz = at_use(F, cur.sample0 >> 31);
+          const Launch& Pz = at_use(P, cur.sample0 >> 31);
+          const uint32_t apix = pix + (Pz.aov_rows ? (rad_row / Pz.aov_rows) * Pz.aov_plane : 0u);
           f3 nd = normalize(r.dir);
-          at_byte(Fz.normal, pix * 12u)[0] = nd.x;
-          at_byte(Fz.normal, pix * 12u)[1] = nd.y;
-          at_byte(Fz.normal, pix * 12u)[2] = nd.z;
-          *at_byte(Fz.depth, pix * 4u) = at_use(C, cur.sample0 >> 31).z_far;
-          *at_byte(Fz.material, pix * 8u) = Sz.sky_id;
+          at_byte(Fz.normal, apix * 12u)[0] = nd.x;
+          at_byte(Fz.normal, apix * 12u)[1] = nd.y;
+          at_byte(Fz.normal, apix * 12u)[2] = nd.z;
+          *at_byte(Fz.depth, apix * 4u) = at_use(C, cur.sample0 >> 31).z_far;
+          *at_byte(Fz.material, apix * 8u) = Sz.sky_id;
         }
         done = true;
       } else {
@@ -1918,11 +1920,13 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
         }
         if (depth == 0 && aov) {
           const DevFrame& Fz = at_use(F, cur.sample0 >> 31);
-          at_byte(Fz.normal, pix * 12u)[0] = nn.x;
-          at_byte(Fz.normal, pix * 12u)[1] = nn.y;
-          at_byte(Fz.normal, pix * 12u)[2] = nn.z;
-          *at_byte(Fz.depth, pix * 4u) = length(r.start - p);
-          *at_byte(Fz.material, pix * 8u) = m.id;
+          const Launch& Pz = at_use(P, cur.sample0 >> 31);
+          const uint32_t apix = pix + (Pz.aov_rows ? (rad_row / Pz.aov_rows) * Pz.aov_plane : 0u);
+          at_byte(Fz.normal, apix * 12u)[0] = nn.x;
+          at_byte(Fz.normal, apix * 12u)[1] = nn.y;
+          at_byte(Fz.normal, apix * 12u)[2] = nn.z;
+          *at_byte(Fz.depth, apix * 4u) = length(r.start - p);
+          *at_byte(Fz.material, apix * 8u) = m.id;
         }
         bool use = mat_will_use(m, refl, nn);
         Ray nr;
@@ -2014,6 +2018,15 @@ __global__ __launch_bounds__(kBlock, WAVES) void render_kernel_lean(DevScene S, 
   }
 }
 
+// A lookahead launch's AOV planes of the folded sample, into the frame.
+__device__ __forceinline__ void fold_aovs(const DevFrame& F, const PathRecords& R, size_t pix) {
+  F.normal[3 * pix] = R.aov_n[3 * pix];
+  F.normal[3 * pix + 1] = R.aov_n[3 * pix + 1];
+  F.normal[3 * pix + 2] = R.aov_n[3 * pix + 2];
+  F.depth[pix] = R.aov_d[pix];
+  F.material[pix] = R.aov_m[pix];
+}
+
 // The backward passes of a launch and their fold into the frame: block b is
 // micro-tile b of group 0 (decode_block's tile-major order without the XCD
 // placement or tile order), lane = pixel; group g's records are row
@@ -2098,6 +2111,7 @@ __global__ __launch_bounds__(kBlock) void fold_paths(DevScene S, DevFrame F, Lau
   F.display[3 * pix] = gamma8(mean.x);
   F.display[3 * pix + 1] = gamma8(mean.y);
   F.display[3 * pix + 2] = gamma8(mean.z);
+  if (R.aov_n) fold_aovs(F, R, pix);
 }
 
 // fold_paths for launches of few micro-tiles (a rank of a multi-GPU render):
@@ -2217,6 +2231,7 @@ __global__ __launch_bounds__(kBlock) void fold_paths_split(DevScene S, DevFrame 
   F.display[3 * pix] = gamma8(mean.x);
   F.display[3 * pix + 1] = gamma8(mean.y);
   F.display[3 * pix + 2] = gamma8(mean.z);
+  if (R.aov_n) fold_aovs(F, R, pix);
 }
 
 // TraceRange (engine.cpp:298-329): one query per lane, the camera ray through
@@ -2347,11 +2362,18 @@ struct DevBuf {
   }
 };
 
-// The lookahead of a 1-spp-style render (fs_options.lookahead): the next
-// call's samples traced in the background on a stream of their own, into
-// their own path records, anchor rows, queues and AOV planes, two slots used
-// in turn so one slot's trace can start while the other's drains.
+// The lookahead of a 1-spp-style render (fs_options.lookahead = w calls):
+// the next w calls' samples traced in the background, in launches of
+// g = max(1, w / 2) calls each (one group per call: a launch of several
+// calls amortizes the latency-bound drain of its last paths), each launch in
+// a slot of its own (stream, path records, anchor rows, queues, per-call AOV
+// planes), so a launch starts while the earlier ones drain. The context
+// stream has the device's highest priority and the slots' streams its
+// lowest, so the folds (on the critical path of the caller's frame) take
+// free wave slots first.
 constexpr uint32_t kLookaheadSpp = 4;
+constexpr uint32_t kLookaheadMax = 8;  // fs_options.lookahead <= 8
+constexpr int kLookSlots = 3;
 struct LookKey {  // everything a lookahead trace depends on
   fs_camera camera;
   fs_render_params params;  // sample_base: the first sample it traces
@@ -2359,15 +2381,21 @@ struct LookKey {  // everything a lookahead trace depends on
   uint64_t scene_gen;
 };
 struct Lookahead {
-  hipStream_t stream[2] = {nullptr, nullptr};
-  hipEvent_t traced[2] = {}, folded[2] = {}, order = nullptr, kev0[2] = {}, kev1[2] = {};
-  DevBuf rows[2], aov[2], queues[2];
-  bool pending[2] = {false, false};
-  bool folded_valid[2] = {false, false};  // folded[i] recorded: the last fold that read slot i
-  LookKey key[2];
-  Launch L[2];
-  PathRecords R[2];
-  int next = 0;
+  hipStream_t stream[kLookSlots] = {};
+  hipEvent_t traced[kLookSlots] = {}, folded[kLookSlots] = {}, order = nullptr, kev0[kLookSlots] = {},
+             kev1[kLookSlots] = {};
+  DevBuf rows[kLookSlots], queues[kLookSlots];
+  // per call (group) the AOV planes of its last sample (normal, depth,
+  // material), which the call's fold copies into the frame
+  DevBuf nrm[kLookSlots], dep[kLookSlots], mid[kLookSlots];
+  uint32_t groups[kLookSlots] = {};  // calls the slot's launch traced (key.params.sample_base: the first)
+  bool pending[kLookSlots] = {};
+  bool folded_valid[kLookSlots] = {};  // folded[i] recorded: the last fold that read slot i
+  LookKey key[kLookSlots];
+  Launch L[kLookSlots];
+  PathRecords R[kLookSlots];
+  uint64_t used[kLookSlots] = {};  // when the slot was last launched (its reuse order)
+  uint64_t tick = 0;
 };
 
 }  // namespace
@@ -2530,7 +2558,7 @@ int carve_records(DevBuf* rows, uint64_t wave_lanes, uint64_t samples, PathRecor
 // Waits for every lookahead trace of the context and drops them (before the
 // scene, the tile order or the context they read is replaced or freed).
 void la_quiesce(fs_context* ctx) {
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < kLookSlots; i++) {
     if (ctx->la.stream[i]) (void)hipStreamSynchronize(ctx->la.stream[i]);
     ctx->la.pending[i] = false;
   }
@@ -2672,7 +2700,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
   else if (o->park_lanes > 64 || o->park_lanes_small > 64) *why = "park_lanes must be 0..64";
   else if (o->lds_rows > 1) *why = "lds_rows must be 0 or 1";
-  else if (o->lookahead > 1) *why = "lookahead must be 0 or 1";
+  else if (o->lookahead > kLookaheadMax) *why = "lookahead must be 0..8";
   else return true;
   return false;
 }
@@ -2793,7 +2821,11 @@ int fs_create(int device, fs_context** out) {
   ctx->device = device;
   fs_options_default(&ctx->opt);
   FS_HIP(hipSetDevice(device));
-  FS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  {  // the highest priority: a fold waiting for wave slots goes before lookahead traces
+    int least = 0, greatest = 0;
+    FS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    FS_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, greatest));
+  }
   FS_HIP(hipEventCreate(&ctx->ev0));
   FS_HIP(hipEventCreate(&ctx->ev1));
   FS_HIP(hipMalloc(&ctx->counters.p, sizeof(DevCounters)));
@@ -2814,9 +2846,9 @@ int fs_destroy(fs_context* ctx) {
   la_quiesce(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < kLookSlots; i++) {
     Lookahead& A = ctx->la;
-    for (DevBuf* b : {&A.rows[i], &A.aov[i], &A.queues[i]}) b->release();
+    for (DevBuf* b : {&A.rows[i], &A.queues[i], &A.nrm[i], &A.dep[i], &A.mid[i]}) b->release();
     for (hipEvent_t e : {A.traced[i], A.folded[i], A.kev0[i], A.kev1[i]})
       if (e) (void)hipEventDestroy(e);
     if (A.stream[i]) (void)hipStreamDestroy(A.stream[i]);
@@ -2856,7 +2888,7 @@ int fs_options_default(fs_options* o) {
   o->build_log = 0;
   o->persist = 1;
   o->small_mesh_tris = 16;
-  o->lookahead = 1;
+  o->lookahead = 8;
   return FS_OK;
 }
 
@@ -3185,14 +3217,20 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // is free (counting the records this context already holds), so a smaller
   // or shared GPU renders in more, smaller launches instead of failing.
   uint64_t row_budget = record_budget(O, 0);
-  {
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-      row_budget = std::min<uint64_t>(row_budget, (free_b + ctx->rows.bytes) / 2);
-  }
   const uint32_t mpt = (ts / 8) * (ts / 8);  // micro-tiles per tile
   Plan plan;
   if ((rc = make_plan(owned, mpt, params->spp, O, row_budget, rec_bytes, &plan))) return rc;
+  // The free-memory cap is queried only for launches of more than 1 GiB of
+  // records (hipMemGetInfo costs the small renders of a window loop a
+  // driver round trip per frame).
+  if ((uint64_t)plan.tiles * mpt * plan.G * plan.chunk * kBlock * rec_bytes > (1ull << 30)) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        (free_b + ctx->rows.bytes) / 2 < row_budget) {
+      row_budget = (free_b + ctx->rows.bytes) / 2;
+      if ((rc = make_plan(owned, mpt, params->spp, O, row_budget, rec_bytes, &plan))) return rc;
+    }
+  }
   ctx->last_launches = 0;
   ctx->last_launch_spp = 0;
   ctx->last_spec = -1;
@@ -3241,25 +3279,44 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     L.tile_order = (const uint32_t*)ctx->tile_order.p;
   }
   // Lookahead (fs_options.lookahead): a whole-frame render of at most
-  // kLookaheadSpp samples in one launch. A pending lookahead of exactly this
-  // call is folded instead of tracing; every other one is dropped (its stream
-  // may still run: it writes only its own slot).
+  // kLookaheadSpp samples in one launch. A pending lookahead slot that traced
+  // exactly this call (as its group g) is folded instead of tracing; slots of
+  // later calls of the same sequence stay; every other one is dropped (its
+  // stream may still run: it writes only its own slot).
   Lookahead& A = ctx->la;
+  // (the per-call AOV planes of a launch must stay within 32-bit byte offsets)
   const bool la_ok = O.lookahead && !count && stride == 1 && params->tile_offset == 0 && O.persist && blocks &&
-                     params->spp <= kLookaheadSpp && plan.parts == 1 && plan.G == 1 && plan.chunk == params->spp;
+                     params->spp <= kLookaheadSpp && plan.parts == 1 && plan.G == 1 && plan.chunk == params->spp &&
+                     (uint64_t)frame->width * frame->height * 12 * (kLookaheadMax / 2) < (1ull << 32);
   LookKey key;
   std::memset(&key, 0, sizeof key);
   int hit = -1;
+  uint32_t hit_group = 0;
+  auto same_sequence = [&](int i) {  // slot i's key but for the first sample
+    LookKey k = A.key[i];
+    k.params.sample_base = params->sample_base;
+    return !std::memcmp(&k, &key, sizeof key);
+  };
   if (la_ok) {
     key.camera = *camera;
     key.params = *params;
     key.opt = O;
     key.scene_gen = ctx->scene_gen;
-    for (int i = 0; i < 2; i++)
-      if (A.pending[i] && !std::memcmp(&A.key[i], &key, sizeof key)) hit = i;
+    for (int i = 0; i < kLookSlots; i++) {
+      const uint32_t b0 = A.key[i].params.sample_base, k = params->sample_base;
+      if (A.pending[i] && k >= b0 && (k - b0) % params->spp == 0 && (k - b0) / params->spp < A.groups[i] &&
+          same_sequence(i)) {
+        hit = i;
+        hit_group = (k - b0) / params->spp;
+      }
+    }
   }
-  for (int i = 0; i < 2; i++)
-    if (i != hit) A.pending[i] = false;
+  for (int i = 0; i < kLookSlots; i++) {
+    if (!A.pending[i]) continue;
+    const uint64_t end = (uint64_t)A.key[i].params.sample_base + (uint64_t)A.groups[i] * A.key[i].params.spp;
+    const bool later = hit >= 0 && end > (uint64_t)params->sample_base + params->spp && same_sequence(i);
+    if (!later) A.pending[i] = false;  // the hit slot too once its last call is folded
+  }
   // On an allocation failure the launches shrink (groups per launch, then
   // tiles per part, then samples per block, each halved) until the records fit.
   while (blocks && hit < 0) {
@@ -3280,26 +3337,38 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // rank's share of a multi-GPU frame), so the serial per-pixel loop is split.
   const uint64_t fold_slots = (uint64_t)ctx->cus * fold_waves_per_cu(fold, fold_lds);
   if (hit >= 0) {
-    // The lookahead traced exactly these samples: its depth-0 AOVs into the
-    // frame, then the fold of its records, after its trace on the other stream.
-    const size_t px = (size_t)frame->width * frame->height;
+    // The lookahead traced exactly these samples as group g of its launch:
+    // the fold of group g's records (the record planes from group g's first
+    // row, as a one-group launch of this call) after the launch's trace on
+    // its stream, copying group g's AOV planes into the frame.
     FS_HIP(hipStreamWaitEvent(ctx->stream, A.traced[hit], 0));
-    FS_HIP(hipMemcpyAsync(frame->normal.p, A.aov[hit].p, 12 * px, hipMemcpyDeviceToDevice, ctx->stream));
-    FS_HIP(hipMemcpyAsync(frame->depth.p, (char*)A.aov[hit].p + 12 * px, 4 * px, hipMemcpyDeviceToDevice, ctx->stream));
-    FS_HIP(hipMemcpyAsync(frame->material.p, (char*)A.aov[hit].p + 16 * px, 8 * px, hipMemcpyDeviceToDevice,
-                          ctx->stream));
-    const Launch& Lh = A.L[hit];
-    const uint64_t pblocks = (uint64_t)Lh.owned * mpt;
+    const size_t px = (size_t)frame->width * frame->height;
+    const uint64_t pblocks = (uint64_t)A.L[hit].owned * mpt;
+    Launch Lh = A.L[hit];
+    Lh.groups = 1;
+    Lh.sample_base = params->sample_base;
+    Lh.nblocks = (uint32_t)pblocks;
+    Lh.aov_rows = Lh.aov_plane = 0;
+    PathRecords Rh = A.R[hit];
+    const uint64_t off = (uint64_t)hit_group * pblocks * Lh.spp * kBlock;
+    Rh.c += off;
+    Rh.ds += off;
+    Rh.end += off;
+    if (Rh.mats) Rh.mats += off;
+    if (Rh.mat) Rh.mat += off;
+    if (Rh.tex) Rh.tex += off;
+    Rh.aov_n = (const float*)A.nrm[hit].p + 3 * px * hit_group;
+    Rh.aov_d = (const float*)A.dep[hit].p + px * hit_group;
+    Rh.aov_m = (const uint64_t*)A.mid[hit].p + px * hit_group;
     const uint32_t fold_log2 = pblocks >= 2 * fold_slots ? 0u : (pblocks >= fold_slots ? 1u : 2u);
     if (fold_log2 == 0)
-      hipLaunchKernelGGL(fold, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, Lh, A.R[hit]);
+      hipLaunchKernelGGL(fold, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, Lh, Rh);
     else
       hipLaunchKernelGGL(fold_split, dim3((uint32_t)(pblocks << fold_log2)), dim3(kBlock), fold_lds, ctx->stream,
-                         ctx->scene, F, Lh, A.R[hit], fold_log2);
+                         ctx->scene, F, Lh, Rh, fold_log2);
     FS_HIP(hipGetLastError());
-    FS_HIP(hipEventRecord(A.folded[hit], ctx->stream));
+    FS_HIP(hipEventRecord(A.folded[hit], ctx->stream));  // the slot's latest reader
     A.folded_valid[hit] = true;
-    A.pending[hit] = false;
     ctx->last_spec = hit;
     ctx->last_launches = 1;
     ctx->last_launch_spp = Lh.spp;
@@ -3341,45 +3410,61 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       FS_HIP(hipGetLastError());
     }
   }
-  // The next call's samples, traced now in the background (slot s, the one
-  // not just folded), unless they would leave the 2^20-sample seed range.
-  if (la_ok && (uint64_t)params->sample_base + 2ull * params->spp <= (1ull << 20)) {
-    const int s = hit >= 0 ? (hit ^ 1) : A.next;
-    A.next = s ^ 1;
+  // The next calls' samples, up to `lookahead` calls ahead, traced now in
+  // the background in launches of g calls into free slots, after what the
+  // pending slots of this sequence already cover; never past the 2^20-sample
+  // seed range.
+  if (la_ok) {
+    const uint32_t spp = params->spp, w = O.lookahead, g = std::max<uint32_t>(1, w / 2);
+    uint64_t cov = (uint64_t)params->sample_base + spp;  // first sample no pending slot traces
+    for (int i = 0; i < kLookSlots; i++)
+      if (A.pending[i]) cov = std::max<uint64_t>(cov, (uint64_t)A.key[i].params.sample_base + (uint64_t)A.groups[i] * spp);
+    const uint64_t want = (uint64_t)params->sample_base + (uint64_t)spp * (1 + w);
     const uint64_t pb = (uint64_t)owned * mpt;
-    const uint64_t grid = grid_for(pb);
+    const uint64_t grid = grid_for(pb * g);
     const size_t px = (size_t)frame->width * frame->height;
-    bool ready = true;
-    if (!A.stream[s]) {
-      FS_HIP(hipStreamCreateWithFlags(&A.stream[s], hipStreamNonBlocking));
-      FS_HIP(hipEventCreateWithFlags(&A.traced[s], hipEventDisableTiming));
-      FS_HIP(hipEventCreateWithFlags(&A.folded[s], hipEventDisableTiming));
-      FS_HIP(hipEventCreate(&A.kev0[s]));
-      FS_HIP(hipEventCreate(&A.kev1[s]));
-      if (!A.order) FS_HIP(hipEventCreateWithFlags(&A.order, hipEventDisableTiming));
-    }
-    const size_t need = rows_bytes(grid * kBlock, pb * params->spp * kBlock, tex_rec, mm);
-    if (A.rows[s].bytes < need || A.aov[s].bytes < 24 * px || !A.queues[s].p) {
-      FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace and fold still use the old buffers
-      FS_HIP(hipStreamSynchronize(ctx->stream));
-      ready = !ensure(&A.rows[s], need) && !ensure(&A.aov[s], 24 * px) &&
-              !ensure(&A.queues[s], 8 * dev::kQueueStride * sizeof(uint32_t));
-      if (!ready) (void)hipGetLastError();  // no room: this call has no lookahead
-    }
-    if (ready && !carve_records(&A.rows[s], grid * kBlock, pb * params->spp * kBlock, &A.R[s], &anchors, tex_rec, mm)) {
+    while (cov < want && cov + (uint64_t)g * spp <= (1ull << 20)) {
+      int s = -1;  // the free slot launched longest ago (its stream's last work is the oldest)
+      for (int i = 0; i < kLookSlots; i++)
+        if (!A.pending[i] && (s < 0 || A.used[i] < A.used[s])) s = i;
+      if (s < 0) break;
+      if (!A.stream[s]) {
+        int least = 0, greatest = 0;
+        FS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        FS_HIP(hipStreamCreateWithPriority(&A.stream[s], hipStreamNonBlocking, least));
+        FS_HIP(hipEventCreateWithFlags(&A.traced[s], hipEventDisableTiming));
+        FS_HIP(hipEventCreateWithFlags(&A.folded[s], hipEventDisableTiming));
+        FS_HIP(hipEventCreate(&A.kev0[s]));
+        FS_HIP(hipEventCreate(&A.kev1[s]));
+        if (!A.order) FS_HIP(hipEventCreateWithFlags(&A.order, hipEventDisableTiming));
+      }
+      const size_t need = rows_bytes(grid * kBlock, pb * g * spp * kBlock, tex_rec, mm);
+      if (A.rows[s].bytes < need || A.nrm[s].bytes < 12 * px * g || A.dep[s].bytes < 4 * px * g ||
+          A.mid[s].bytes < 8 * px * g || !A.queues[s].p) {
+        FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace and folds still use the old buffers
+        FS_HIP(hipStreamSynchronize(ctx->stream));
+        if (ensure(&A.rows[s], need) || ensure(&A.nrm[s], 12 * px * g) || ensure(&A.dep[s], 4 * px * g) ||
+            ensure(&A.mid[s], 8 * px * g) || ensure(&A.queues[s], 8 * dev::kQueueStride * sizeof(uint32_t))) {
+          (void)hipGetLastError();  // no room: no (further) lookahead for this call
+          break;
+        }
+      }
+      if (carve_records(&A.rows[s], grid * kBlock, pb * g * spp * kBlock, &A.R[s], &anchors, tex_rec, mm)) break;
       Launch Ls = L;
       Ls.owned = owned;
       Ls.tile_offset = 0;
-      Ls.sample_base = params->sample_base + params->spp;
-      Ls.spp = params->spp;
-      Ls.groups = 1;
-      Ls.nblocks = (uint32_t)pb;
-      DevFrame Fs{};  // the trace writes only the last sample's AOVs: into the slot's planes
+      Ls.sample_base = (uint32_t)cov;
+      Ls.spp = spp;
+      Ls.groups = g;
+      Ls.nblocks = (uint32_t)(pb * g);
+      Ls.aov_rows = (uint32_t)pb;  // group k's AOVs in plane k
+      Ls.aov_plane = (uint32_t)px;
+      DevFrame Fs{};  // the trace writes only the AOVs: into the slot's planes
       Fs.width = frame->width;
       Fs.height = frame->height;
-      Fs.normal = (float*)A.aov[s].p;
-      Fs.depth = (float*)((char*)A.aov[s].p + 12 * px);
-      Fs.material = (uint64_t*)((char*)A.aov[s].p + 16 * px);
+      Fs.normal = (float*)A.nrm[s].p;
+      Fs.depth = (float*)A.dep[s].p;
+      Fs.material = (uint64_t*)A.mid[s].p;
       if (A.folded_valid[s]) FS_HIP(hipStreamWaitEvent(A.stream[s], A.folded[s], 0));  // its records' last reader
       if (order_copied) {
         FS_HIP(hipEventRecord(A.order, ctx->stream));
@@ -3395,7 +3480,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       A.L[s] = Ls;
       A.key[s] = key;
       A.key[s].params.sample_base = Ls.sample_base;
+      A.groups[s] = g;
       A.pending[s] = true;
+      A.used[s] = ++A.tick;
+      cov += (uint64_t)g * spp;
     }
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));

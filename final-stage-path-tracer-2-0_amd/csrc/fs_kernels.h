@@ -101,6 +101,11 @@ struct PathRecords {
   uint32_t* mat;   // [level][q]: the material id of every level (MMAT), else null
   float4* tex;     // [level][q]: SampleDiffuse's texel of a textured material (TEX), else null
   uint64_t n;      // samples of the launch (the level stride)
+  // fold_paths only: the AOV planes a lookahead launch wrote for the samples
+  // it folds (fs_options.lookahead), copied into the frame; null otherwise
+  const float* aov_n;
+  const float* aov_d;
+  const uint64_t* aov_m;
 };
 // PathRecords::end.w flag: level 0 is Fog and its draw took the diffuse colour
 constexpr uint32_t kRecFogDif = 0x100u;
@@ -130,6 +135,11 @@ struct Launch {
   uint64_t seed;
   uint32_t nblocks;  // blocks of the launch: owned tiles x micro-tiles x groups
   uint32_t persist;  // 1: persistent waves pull blocks from per-XCD queues; 0: one wave per block
+  // Lookahead launches (one sample per group, each group a later TraceScene
+  // call): every group's sample leaves its AOVs, group g in plane g, at
+  // pixel offset g x aov_plane (group g = record row / aov_rows). 0: only
+  // the last group's last sample writes the frame's AOV planes.
+  uint32_t aov_rows, aov_plane;
 };
 
 }  // namespace fs

@@ -1126,14 +1126,21 @@ void TraceSceneBatch(const Camera& view, Scene* scene, DisplayFrame* output, uin
     have += n;
     left -= n;
   }
-  int rc = fs_synchronize(e.ctx);
-  if (rc) {
-    engine_fail(e, rc, "fs_synchronize");
-    return;
+  // The frame's accessors (GetDisplayBuffer & co.) read it on the same
+  // stream, so the call returns once its work is enqueued; it waits for the
+  // device only to time the frame for the reference's log line (the window
+  // loop then overlaps this frame's fold with the host's previous display).
+  const bool timed = !view.fast_render_enabled && e.settings.timing_log;
+  if (timed) {
+    int rc = fs_synchronize(e.ctx);
+    if (rc) {
+      engine_fail(e, rc, "fs_synchronize");
+      return;
+    }
   }
   output->add_samples(spp);
   double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (!view.fast_render_enabled && e.settings.timing_log)  // engine.cpp:284-293
+  if (timed)  // engine.cpp:284-293
     std::printf("Frame %u render time: %.2f sec. Msamples/sec: %.2f\n", e.frame_counter, sec,
                 (double)p.width * p.height * spp / (1e6 * sec));
   e.frame_counter++;

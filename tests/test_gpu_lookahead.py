@@ -61,9 +61,11 @@ def test_lookahead_loop_bit_exact(name, spp, scene_dir, gpu_renderer):
 
 
 def test_lookahead_discarded_when_the_call_changes(scene_dir, gpu_renderer):
-    """A camera change, a frame reset, a skipped sample index and a lens
-    camera between calls: each such call traces anew (no fold), and the frame
-    is the oracle's for the same call sequence."""
+    """A camera change, a skipped sample index and a lens camera between
+    calls: a call that changes the camera traces anew (no fold); a skip of
+    one sample index still finds the lookahead (8 calls ahead by default, one
+    call with lookahead 1 misses it); a frame reset keeps it. Every frame is
+    the oracle's for the same call sequence."""
     s = load_scene("c2", scene_dir)
     a = s.camera(0)
     b = fsamd.camera((2, 9, -30), (0, 10, 0), fov_y=44, aperture=0.0)
@@ -72,7 +74,12 @@ def test_lookahead_discarded_when_the_call_changes(scene_dir, gpu_renderer):
     f = gpu_renderer.frame(W, H)
     steps = [(a, 1, 0), (a, 1, 1), (b, 1, 2), (b, 1, 3), (b, 1, 5), (b, 1, 6), (lens, 1, 7), (lens, 1, 8)]
     folded = gpu_seq(gpu_renderer, f, steps)
-    assert folded == [False, True, False, True, False, True, False, True]
+    assert folded == [False, True, False, True, True, True, False, True]
+    gpu_renderer.set_options(lookahead=1)  # depth 1: the skip misses
+    folded = gpu_seq(gpu_renderer, f, [(a, 1, 9), (a, 1, 10), (a, 1, 12), (a, 1, 13)])
+    assert folded == [False, True, False, True]
+    steps += [(a, 1, 9), (a, 1, 10), (a, 1, 12), (a, 1, 13)]
+    gpu_renderer.set_options(lookahead=2)
     out = planes(f)
     assert_parity(out, oracle_seq(s.desc_ptr(), steps), exact=True)
     # a reset between two calls of the same sequence: the fold goes into the reset frame
@@ -128,3 +135,25 @@ def test_frame_map_is_the_plane(scene_dir, gpu_renderer):
     for p in range(6):
         np.testing.assert_array_equal(f.map(p), f.read(p))
     f.close()
+
+
+def test_lookahead_full_width_fold_bit_exact(scene_dir, gpu_renderer):
+    """A frame large enough for the one-lane-per-pixel fold (fold_paths, not
+    the split fold of small frames): four calls, the last three folded from
+    one lookahead launch of four calls, every plane the oracle's."""
+    s = load_scene("c2", scene_dir)
+    cam = s.camera(0)
+    gpu_renderer.upload(s)
+    w, h = 1024, 960
+    f = gpu_renderer.frame(w, h)
+    folded = []
+    for k in range(4):
+        gpu_renderer.render(cam, f, spp=1, sample_base=k)
+        folded.append(gpu_renderer.last_lookahead())
+    assert folded == [False, True, True, True]
+    out = planes(f)
+    f.close()
+    o = oracle_py.Scene(s.desc_ptr())
+    ref = o.render(cam, fsamd.render_params(w, h, 4), threads=16)
+    o.close()
+    assert_parity(out, ref, exact=True)

@@ -1,8 +1,10 @@
-"""Per-frame time split of the drop-in window loop (examples/dropin_rate under
+"""Per-frame timeline of the drop-in window loop (examples/dropin_rate under
 rocprofv3 --kernel-trace --memory-copy-trace): for each displayed frame the
-trace kernel, fold_paths, fills, the display copy and the gaps between them
-(host round trips), medians over the loop's frames (measurement aid, DESIGN
-§6). usage: python tools/dropin_split.py PROFILE_DIR"""
+fold of its samples, the display copy to the host and the gaps between them,
+and how the trace that made the samples lines up with its fold (with the
+lookahead, fs_options.lookahead, traces run ahead of their folds on other
+streams). Medians over the loop's frames, in us (measurement aid, DESIGN §6;
+VERDICT r5 item 3). usage: python tools/dropin_split.py PROFILE_DIR"""
 import csv
 import glob
 import os
@@ -18,45 +20,48 @@ def rows(pattern, root):
     return out
 
 
-def classify(name):
-    if name.startswith("render_kernel") or "render_kernel_lean" in name:
-        return "trace"
-    if "fold_paths" in name:
-        return "fold"
-    if "fill" in name.lower() or "memset" in name.lower():
-        return "fill"
-    return "other"
-
-
 def main(root):
-    ev = []
+    traces, folds, copies = [], [], []
     for r in rows("*kernel_trace.csv", root):
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), classify(r["Kernel_Name"]), r["Kernel_Name"]))
+        ev = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+        if "render_kernel_lean" in r["Kernel_Name"]:
+            traces.append(ev)
+        elif "fold_paths" in r["Kernel_Name"]:
+            folds.append(ev)
     for r in rows("*memory_copy_trace.csv", root):
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy_" + r.get("Direction", "?"), "copy"))
-    ev.sort()
-    # frames: each starts at a trace-kernel launch of one 1-spp frame; the last
-    # trace launches belong to the batched submission and are dropped with it
-    starts = [i for i, e in enumerate(ev) if e[2] == "trace"]
-    if len(starts) < 8:
-        raise SystemExit(f"only {len(starts)} trace launches in {root}")
+        if "DEVICE_TO_HOST" in r.get("Direction", ""):
+            copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    traces.sort()
+    folds.sort()
+    copies.sort()
+    if len(folds) < 8:
+        raise SystemExit(f"only {len(folds)} folds in {root}")
+    # frame k: fold k and the first display copy after it; the k-th trace made
+    # its samples (traces start in sample order). Skip the warm-up frame and
+    # the batched submission at the end (its fold has no copy before the last).
     frames = []
-    for a, b in zip(starts[1:-2], starts[2:-1]):  # skip the warm-up frame and the batch tail
-        seg = ev[a:b]
-        d = {}
-        for s, e, k, _ in seg:
-            d[k] = d.get(k, 0) + (e - s)
-        d["period"] = ev[b][0] - ev[a][0]
-        d["busy"] = sum(e - s for s, e, _, _ in seg)
-        d["gaps"] = d["period"] - d["busy"]
+    ci = 0
+    for k in range(1, len(folds) - 2):
+        fs, fe = folds[k]
+        while ci < len(copies) and copies[ci][0] < fe:
+            ci += 1
+        if ci >= len(copies):
+            break
+        cs, ce = copies[ci]
+        nxt = folds[k + 1][0]
+        d = {"period": nxt - fs, "fold": fe - fs, "fold_to_copy": cs - fe, "copy": ce - cs,
+             "copy_to_next_fold": nxt - ce}
+        if k < len(traces):
+            ts, te = traces[k]
+            d["trace"] = te - ts
+            d["trace_end_to_fold_start"] = fs - te  # > 0: the fold did not wait for its trace
         frames.append(d)
-    keys = sorted({k for f in frames for k in f})
-    print(f"# {len(frames)} frames from {root}; medians in us")
-    for k in keys:
-        vals = [f.get(k, 0) / 1e3 for f in frames]
-        print(f"{k:>16}: {statistics.median(vals):9.1f}  (min {min(vals):.1f}, max {max(vals):.1f})")
-    names = sorted({n for _, _, k, n in ev if k in ("trace", "fold")})
-    print("kernels:", "; ".join(names))
+    print(f"# {len(frames)} frames from {root}; medians in us (min, max)")
+    for key in ("period", "fold", "fold_to_copy", "copy", "copy_to_next_fold", "trace", "trace_end_to_fold_start"):
+        vals = [f[key] / 1e3 for f in frames if key in f]
+        if vals:
+            print(f"{key:>24}: {statistics.median(vals):9.1f}  ({min(vals):.1f}, {max(vals):.1f})")
+    print(f"traces {len(traces)}, folds {len(folds)}, display copies {len(copies)}")
 
 
 if __name__ == "__main__":

@@ -13,6 +13,8 @@
 #   ab:VARIANTS:SCENES:SPP:ROUNDS   tools/perf_ab.py (fs_options A/B in one process)
 #   libab:LIBS:SCENES:SPP:ROUNDS    alternating processes over in-tree builds (space-separated .so names)
 #   wt[:SCENES[:SPPS]]           per-wave end/drain times of the trace kernel (needs libfsgpu_wt.so)
+#   dropin:SCENE:FRAMES[:DEPTHS]  examples/dropin_rate (the reference's window loop) at each lookahead depth
+#                                ("0 1 2"; default the library's), then a kernel + copy trace of the default
 #   phase:SCENES:SPP             per-phase cycle split (needs the in-tree libfsgpu_prof.so)
 #   lib:NAME                     the steps after it load final-stage-path-tracer-2-0_amd/NAME (an A/B build)
 #                                through FSAMD_GPU_LIB; "lib:" alone returns to the product libfsgpu.so
@@ -98,11 +100,14 @@ for step in "$@"; do
     dropin)
       # the reference's window loop through the C++ mirror (examples/dropin_rate), then the same
       # loop under a kernel + memory-copy trace (per-frame split: trace, fold, copies, gaps)
-      sc=${a1:-c4}; n=${a2:-256}
+      sc=${a1:-c4}; n=${a2:-256}; la=${a3:-}
       p=$(python3 -c "import sys; sys.path.insert(0, 'final-stage-path-tracer-2-0_amd'); import scenes; print(scenes.write('$sc', '/tmp/fs_scenes/$sc'))") \
         || fail "$step" $?
-      timeout -k 10 300 ./examples/dropin_rate $p 1920 1080 $n > $OUT/dropin_${sc}_1920x1080.json \
-        2> $OUT/dropin_$sc.err || fail "$step" $? $OUT/dropin_$sc.err
+      for d in ${la:-default}; do
+        [ "$d" = default ] && d=
+        timeout -k 10 300 ./examples/dropin_rate $p 1920 1080 $n $d >> $OUT/dropin_${sc}_1920x1080.json \
+          2> $OUT/dropin_$sc.err || fail "$step" $? $OUT/dropin_$sc.err
+      done
       cat $OUT/dropin_${sc}_1920x1080.json
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
         -d $OUT/dropin_prof_$sc -o trace -- ./examples/dropin_rate $p 1920 1080 64 > $OUT/dropin_prof_$sc.json \
