@@ -6,7 +6,9 @@
 // Scene load and BVH build are excluded (one warm-up frame first).
 //
 //   dropin_rate <file.scene> <width> <height> <frames> [lookahead depth, default the library's]
+#include <algorithm>
 #include <chrono>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 
@@ -47,10 +49,13 @@ int main(int argc, char** argv) {
     return 1;
   }
   // the window loop: one TraceScene (1 spp) and one display read per frame
+  std::vector<double> per(frames);
   double t0 = now_s();
   for (unsigned i = 0; i < frames; i++) {
+    const double tf = now_s();
     base::TraceScene(camera, &scene, &frame);
     frame.GetDisplayBuffer();
+    per[i] = now_s() - tf;
     if (base::LastTraceStatus() != 0) {  // a failed frame must not count as rendered
       std::fprintf(stderr, "frame %u failed: %s\n", i, base::LastTraceError());
       return 1;
@@ -68,9 +73,12 @@ int main(int argc, char** argv) {
     return 1;
   }
   const double samples = (double)W * H * frames;
+  std::sort(per.begin(), per.end());
+  auto pct = [&](double q) { return per[std::min<size_t>(per.size() - 1, (size_t)(q * per.size()))] * 1e3; };
   std::printf("{\"width\": %u, \"height\": %u, \"frames\": %u, \"lookahead\": %u, \"loop_msamples_per_s\": %.2f, "
-              "\"loop_ms_per_frame\": %.3f, \"batch_msamples_per_s\": %.2f}\n",
+              "\"loop_ms_per_frame\": %.3f, \"frame_ms_p10_p50_p90_max\": [%.3f, %.3f, %.3f, %.3f], "
+              "\"batch_msamples_per_s\": %.2f}\n",
               W, H, frames, base::GetTraceSettings().options.lookahead, samples / loop_s / 1e6, loop_s * 1e3 / frames,
-              samples / batch_s / 1e6);
+              pct(0.1), pct(0.5), pct(0.9), per.back() * 1e3, samples / batch_s / 1e6);
   return 0;
 }

@@ -2364,7 +2364,7 @@ struct DevBuf {
 
 // The lookahead of a 1-spp-style render (fs_options.lookahead = w calls):
 // the next w calls' samples traced in the background, in launches of
-// g = max(1, w / 2) calls each (one group per call: a launch of several
+// g = min(16, max(1, w / 3)) calls each (one group per call: a launch of several
 // calls amortizes the latency-bound drain of its last paths), each launch in
 // a slot of its own (stream, path records, anchor rows, queues, per-call AOV
 // planes), so a launch starts while the earlier ones drain. The context
@@ -2372,7 +2372,8 @@ struct DevBuf {
 // lowest, so the folds (on the critical path of the caller's frame) take
 // free wave slots first.
 constexpr uint32_t kLookaheadSpp = 4;
-constexpr uint32_t kLookaheadMax = 8;  // fs_options.lookahead <= 8
+constexpr uint32_t kLookaheadMax = 48;  // fs_options.lookahead <= 48
+constexpr uint32_t kLookGroupMax = 16;  // calls per lookahead launch
 constexpr int kLookSlots = 3;
 struct LookKey {  // everything a lookahead trace depends on
   fs_camera camera;
@@ -2396,6 +2397,11 @@ struct Lookahead {
   PathRecords R[kLookSlots];
   uint64_t used[kLookSlots] = {};  // when the slot was last launched (its reuse order)
   uint64_t tick = 0;
+  // the slots of the last two launches, newest first (-1: none): a launch
+  // starts only once the launch two before it has finished, so it takes the
+  // wave slots the previous launch frees as it drains and never shares the
+  // chip with the launch the caller needs next
+  int prev[2] = {-1, -1};
 };
 
 }  // namespace
@@ -2700,7 +2706,7 @@ bool valid_options(const fs_options* o, std::string* why) {
   else if (o->small_mesh_tris > kMaxSmallMeshTris) *why = "small_mesh_tris must be 0..64";
   else if (o->park_lanes > 64 || o->park_lanes_small > 64) *why = "park_lanes must be 0..64";
   else if (o->lds_rows > 1) *why = "lds_rows must be 0 or 1";
-  else if (o->lookahead > kLookaheadMax) *why = "lookahead must be 0..8";
+  else if (o->lookahead > kLookaheadMax) *why = "lookahead must be 0..48";
   else return true;
   return false;
 }
@@ -2888,7 +2894,7 @@ int fs_options_default(fs_options* o) {
   o->build_log = 0;
   o->persist = 1;
   o->small_mesh_tris = 16;
-  o->lookahead = 8;
+  o->lookahead = 12;
   return FS_OK;
 }
 
@@ -3287,7 +3293,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // (the per-call AOV planes of a launch must stay within 32-bit byte offsets)
   const bool la_ok = O.lookahead && !count && stride == 1 && params->tile_offset == 0 && O.persist && blocks &&
                      params->spp <= kLookaheadSpp && plan.parts == 1 && plan.G == 1 && plan.chunk == params->spp &&
-                     (uint64_t)frame->width * frame->height * 12 * (kLookaheadMax / 2) < (1ull << 32);
+                     (uint64_t)frame->width * frame->height * 12 < (1ull << 32);
   LookKey key;
   std::memset(&key, 0, sizeof key);
   int hit = -1;
@@ -3317,6 +3323,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     const bool later = hit >= 0 && end > (uint64_t)params->sample_base + params->spp && same_sequence(i);
     if (!later) A.pending[i] = false;  // the hit slot too once its last call is folded
   }
+  if (hit < 0) A.prev[0] = A.prev[1] = -1;  // a new sequence: no launch to queue behind
   // On an allocation failure the launches shrink (groups per launch, then
   // tiles per part, then samples per block, each halved) until the records fit.
   while (blocks && hit < 0) {
@@ -3415,7 +3422,13 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // pending slots of this sequence already cover; never past the 2^20-sample
   // seed range.
   if (la_ok) {
-    const uint32_t spp = params->spp, w = O.lookahead, g = std::max<uint32_t>(1, w / 2);
+    // g calls per launch: w / 3, so three slots hold the window; at most
+    // kLookGroupMax, and fewer where the per-call AOV planes would pass the
+    // 32-bit byte offsets of the trace kernel's AOV stores
+    const uint64_t pxl = (uint64_t)frame->width * frame->height;
+    const uint32_t spp = params->spp, w = O.lookahead,
+                   g = (uint32_t)std::min<uint64_t>({kLookGroupMax, std::max<uint32_t>(1, w / 3),
+                                                     ((1ull << 32) - 1) / (12 * pxl)});
     uint64_t cov = (uint64_t)params->sample_base + spp;  // first sample no pending slot traces
     for (int i = 0; i < kLookSlots; i++)
       if (A.pending[i]) cov = std::max<uint64_t>(cov, (uint64_t)A.key[i].params.sample_base + (uint64_t)A.groups[i] * spp);
@@ -3470,6 +3483,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         FS_HIP(hipEventRecord(A.order, ctx->stream));
         FS_HIP(hipStreamWaitEvent(A.stream[s], A.order, 0));
       }
+      if (A.prev[1] >= 0 && A.prev[1] != s) FS_HIP(hipStreamWaitEvent(A.stream[s], A.traced[A.prev[1]], 0));
       FS_HIP(hipMemsetAsync(A.queues[s].p, 0, A.queues[s].bytes, A.stream[s]));
       FS_HIP(hipEventRecord(A.kev0[s], A.stream[s]));
       hipLaunchKernelGGL(K.fn, dim3((uint32_t)grid), dim3(kBlock), 0, A.stream[s], ctx->scene, C, Fs, Ls, A.R[s],
@@ -3483,6 +3497,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       A.groups[s] = g;
       A.pending[s] = true;
       A.used[s] = ++A.tick;
+      A.prev[1] = A.prev[0];
+      A.prev[0] = s;
       cov += (uint64_t)g * spp;
     }
   }

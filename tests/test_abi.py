@@ -49,7 +49,7 @@ def test_options_defaults_and_validation_without_device():
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
                  "small_mesh_tris": 16, "park_lanes_small": 6,
-                 "lds_rows": 1, "record_budget_mb": 0, "lookahead": 8}
+                 "lds_rows": 1, "record_budget_mb": 0, "lookahead": 12}
     assert fsamd.parse_variant("schedule=parked@park_lanes=8") == {"schedule": "parked", "park_lanes": 8}
     assert fsamd.options(schedule="parked").schedule == 2
     lib = fsamd.gpu_lib()
@@ -58,7 +58,7 @@ def test_options_defaults_and_validation_without_device():
     d, n = C.c_uint64(), C.c_uint64()
     for bad in ({"bvh_leaf": 0}, {"bvh_leaf": 16}, {"bvh_bins": 65}, {"samples_per_block": 65}, {"schedule": 3}, {"xcd_bands": 3},
                 {"persist": 2}, {"small_mesh_tris": 65}, {"park_lanes": 65}, {"lds_rows": 2},
-                {"lookahead": 9}):
+                {"lookahead": 49}):
         ob = fsamd.options(**bad)
         assert lib.fs_prepare_digest(C.c_void_p(1), C.byref(ob), C.byref(d), C.byref(n), None) == -1, bad
     with pytest.raises(fsamd.FsError):
