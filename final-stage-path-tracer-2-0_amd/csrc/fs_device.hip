@@ -1004,7 +1004,7 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& S, uint32_t root, in
       // top. Unconditional, so in bounds only because sp <= this node's depth
       // < kTraversalStack: both builders stop splitting at depth
       // kTraversalStack - 1 (fs_scene.cpp split depth rule, kGuard in
-      // fs_bvh_gpu.hip; tests/test_gpu_bvh.py deep-mesh case).
+      // fs_bvh_gpu.hip; tests/test_abi.py deep-mesh case).
       static_assert(kTraversalStack >= 2, "the walk stack holds the root's far child");
       stk[sp * kBlock] = far;
       const uint32_t w1 = any ? near : (sp > 0 ? top1 : kNone);

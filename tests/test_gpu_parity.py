@@ -676,6 +676,40 @@ def test_c5_2160p_shards_equal_single_gpu(scene_dir, gpu_renderer):
     part.close()
 
 
+def test_c5_2160p_rank_tiles_match_oracle(scene_dir, gpu_renderer):
+    """the 2160p shard tests compare the GPU with itself.
+    Here one rank's tiles of a 61-rank partition of the C4 scene at
+    3840 x 2160 (34 tiles of 64 x 64, tile_offset 7, as the multi-GPU
+    render deals them) at 4 spp, GPU against the oracle: the sample-count
+    plane exact, colour within the stated tolerance (the reference octree's
+    rare split-plane misses), the differing pixels recorded."""
+    r = gpu_renderer
+    s = load_scene("c4", scene_dir)
+    cam = s.camera(0)
+    r.upload(s, gpu_bvh=True)
+    W, H, spp, off, stride = 3840, 2160, 4, 7, 61
+    f = r.frame(W, H)
+    r.render(cam, f, spp=spp, tile_offset=off, tile_stride=stride)
+    out = {p: f.read(p) for p in range(6)}
+    f.close()
+    ref = oracle_render(s.desc_ptr(), cam, W, H, spp, tile_offset=off, tile_stride=stride)
+    owned = ref.count > 0
+    tiles = [t for t in range(60 * 34) if t % stride == off]  # 64 x 64 tiles, the last row 48 high
+    assert owned.sum() == sum(64 * min(64, H - (t // 60) * 64) for t in tiles)
+    np.testing.assert_array_equal(out[fsamd.PLANE_COUNT], ref.count)
+    diff = {}
+    for p, rp in ((fsamd.PLANE_COLOR, ref.color), (fsamd.PLANE_DISPLAY, ref.display), (fsamd.PLANE_NORMAL, ref.normal),
+                  (fsamd.PLANE_DEPTH, ref.depth), (fsamd.PLANE_MATERIAL, ref.material)):
+        bad = out[p] != rp
+        diff[p] = int((bad.any(axis=-1) if bad.ndim == 3 else bad).sum())
+    _record("c5_rank_tiles_parity", {"W": W, "H": H, "spp": spp, "tile_offset": off, "tile_stride": stride,
+                                     "pixels": int(owned.sum()), "pixels_differing_per_plane": diff})
+    gc, rc = out[fsamd.PLANE_COLOR][owned], ref.color[owned]
+    d = np.abs(gc.astype(np.float64) - rc)
+    assert (d <= 1e-3 + 1e-2 * np.abs(rc)).mean() >= 0.999
+    assert diff[fsamd.PLANE_MATERIAL] <= 1e-3 * owned.sum(), diff
+
+
 # ---- every fs_options setting renders the same frame -----------------------
 OPTION_VARIANTS = [
     {},
