@@ -7,6 +7,7 @@
 #   smoke                        __graft_entry__.smoke()
 #   bench:SCENE[:WxH[:STEPS]]    one bench.py line -> bench_SCENE_WxH.json (C4 1080p adds the CPU baseline)
 #   prof[:SCENE]                 rocprofv3 --kernel-trace --stats of the bench command -> prof_SCENE/
+#   flips:SCENE[:WxH[:SPP]]      tools/flip_hunt.py: GPU frame against the oracle, every differing pixel
 #   sweep[:SCENES]               tools/spp_sweep.py: one launch's trace time against its samples
 #   pmc:SCENE:WxH:SPP[:STEPS]    PMC passes (one counter group each) + tools/pmc_summary.py
 #                                -> pmc_SCENE_WxH.json, stamped with the code object's digest
@@ -80,6 +81,11 @@ for step in "$@"; do
       python3 tools/pmc_summary.py $d "$kern" $d.json "$sc ${wh} x $spp spp in launches of $lspp spp" \
         $((w * h * lspp)) > $d/summary.log 2>&1 || fail "$step" $? $d/summary.log
       grep -E "hbm_bytes_per_sample|valu_lane_util|wait_any|valu_issue|code_object" $d.json ;;
+    flips)
+      sc=$a1; wh=${a2:-1920x1080}; w=${wh%x*}; h=${wh#*x}; spp=${a3:-4}
+      timeout -k 10 900 python3 tools/flip_hunt.py $sc $w $h $spp $OUT/flips_${sc}_${wh}x${spp}.json \
+        > $OUT/flips_${sc}_${wh}x${spp}.log 2>&1 || fail "$step" $? $OUT/flips_${sc}_${wh}x${spp}.log
+      head -3 $OUT/flips_${sc}_${wh}x${spp}.log ;;
     sweep)
       timeout -k 10 600 python3 tools/spp_sweep.py ${a1:-c4,c2} > $OUT/spp_sweep.log 2>&1 || fail "$step" $? $OUT/spp_sweep.log
       cat $OUT/spp_sweep.log ;;
