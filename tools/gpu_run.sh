@@ -14,6 +14,7 @@
 #   ab:VARIANTS:SCENES:SPP:ROUNDS   tools/perf_ab.py (fs_options A/B in one process)
 #   libab:LIBS:SCENES:SPP:ROUNDS    alternating processes over in-tree builds (space-separated .so names)
 #   wt[:SCENES[:SPPS]]           per-wave end/drain times of the trace kernel (needs libfsgpu_wt.so)
+#   dropinlib:LIB:SCENE[:FRAMES[:DEPTH]]  the same window loop on an A/B build of libfsgpu.so
 #   dropin:SCENE:FRAMES[:DEPTHS]  examples/dropin_rate (the reference's window loop) at each lookahead depth
 #                                ("0 1 2"; default the library's), then a kernel + copy trace of the default
 #   phase:SCENES:SPP             per-phase cycle split (needs the in-tree libfsgpu_prof.so)
@@ -103,6 +104,18 @@ for step in "$@"; do
         done
       done
       grep -E "^==|variant|md5" $log ;;
+    dropinlib)
+      # the window loop on an A/B build: its libfsgpu.so (with the product libfshost.so) first on
+      # the library path (the examples' RUNPATH yields to LD_LIBRARY_PATH)
+      lib=$a1; sc=${a2:-c4}; n=${a3:-256}
+      d=/tmp/fs_ablib_${lib%.so}; mkdir -p $d
+      cp final-stage-path-tracer-2-0_amd/$lib $d/libfsgpu.so && cp final-stage-path-tracer-2-0_amd/libfshost.so $d/ \
+        || fail "$step" $?
+      p=$(python3 -c "import sys; sys.path.insert(0, 'final-stage-path-tracer-2-0_amd'); import scenes; print(scenes.write('$sc', '/tmp/fs_scenes/$sc'))") \
+        || fail "$step" $?
+      LD_LIBRARY_PATH=$d timeout -k 10 300 ./examples/dropin_rate $p 1920 1080 $n ${a4:-} >> $OUT/dropin_${sc}_${lib%.so}.json \
+        2> $OUT/dropin_${sc}_${lib%.so}.err || fail "$step" $? $OUT/dropin_${sc}_${lib%.so}.err
+      tail -1 $OUT/dropin_${sc}_${lib%.so}.json ;;
     dropin)
       # the reference's window loop through the C++ mirror (examples/dropin_rate), then the same
       # loop under a kernel + memory-copy trace (per-frame split: trace, fold, copies, gaps)
