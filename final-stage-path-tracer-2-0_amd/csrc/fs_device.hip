@@ -2114,6 +2114,60 @@ __global__ __launch_bounds__(kBlock) void fold_paths(DevScene S, DevFrame F, Lau
   if (R.aov_n) fold_aovs(F, R, pix);
 }
 
+// fold_paths without its cross-sample load pipeline: the fold of a
+// lookahead launch's call (one sample per pixel, or a few), which runs while
+// the next lookahead launch traces. With fewer registers (45-55 VGPRs against
+// fold_paths' 66-80) it fits beside more background trace waves (bg_waves).
+// The same backward passes and fold in sample order as fold_paths.
+template <bool TEX, bool MMAT, bool LDSM>
+__global__ __launch_bounds__(kBlock) void fold_paths_lite(DevScene S, DevFrame F, Launch P, PathRecords R) {
+  extern __shared__ float4 mat_lds[];
+  const uint32_t lane = threadIdx.x, b = blockIdx.x;
+  if (LDSM) {
+    for (uint32_t i = lane; i < 3 * S.num_materials; i += kBlock) mat_lds[i] = S.umat[i];
+    __syncthreads();
+  }
+  const uint32_t micro_per_side = P.tile_size / 8, micro_per_tile = micro_per_side * micro_per_side;
+  const uint32_t owned = b / micro_per_tile, micro = b % micro_per_tile;
+  const uint32_t tile = P.tile_offset + owned * P.tile_stride;
+  const uint32_t x = (tile % P.tiles_x) * P.tile_size + (micro % micro_per_side) * 8 + (lane & 7);
+  const uint32_t y = (tile / P.tiles_x) * P.tile_size + (micro / micro_per_side) * 8 + (lane >> 3);
+  if (x >= F.width || y >= F.height) return;
+  const size_t pix = (size_t)y * F.width + x;
+  f3 mean = mk3(F.color[3 * pix], F.color[3 * pix + 1], F.color[3 * pix + 2]);
+  uint32_t n = F.count[pix];
+  const uint32_t total = P.groups * P.spp;
+  const uint2 none = make_uint2(0u, 0u);
+  for (uint32_t i = 0; i < total; i++) {
+    const uint32_t g = i / P.spp, k = i - g * P.spp;
+    const uint64_t q = rec_index(P, g * gridDim.x + b, k * kBlock + lane);
+    const float4 e = R.end[q];
+    const uint2 m = MMAT ? none : R.mats[q];
+    const uint32_t meta = __float_as_uint(e.w);
+    const int top = (int)(meta & 0xFFu) - 1;
+    float c[kMaxDepth];
+#pragma unroll
+    for (int l = 0; l < (int)kMaxDepth; l++) c[l] = l <= top ? R.c[(uint64_t)l * R.n + q] : 0.0f;
+    f3 L;
+    if (LDSM)
+      L = unwind_path<TEX, MMAT>(static_cast<const float4*>(mat_lds), R, q, mk3(e.x, e.y, e.z), top,
+                                 (meta & kRecFogDif) != 0, m, c);
+    else
+      L = unwind_path<TEX, MMAT>(S.umat, R, q, mk3(e.x, e.y, e.z), top, (meta & kRecFogDif) != 0, m, c);
+    f3 np = mean * (float)n + L;
+    float dv = (float)(++n);
+    mean = mk3(np.x / dv, np.y / dv, np.z / dv);
+  }
+  F.color[3 * pix] = mean.x;
+  F.color[3 * pix + 1] = mean.y;
+  F.color[3 * pix + 2] = mean.z;
+  F.count[pix] = n;
+  F.display[3 * pix] = gamma8(mean.x);
+  F.display[3 * pix + 1] = gamma8(mean.y);
+  F.display[3 * pix + 2] = gamma8(mean.z);
+  if (R.aov_n) fold_aovs(F, R, pix);
+}
+
 // fold_paths for launches of few micro-tiles (a rank of a multi-GPU render):
 // the same backward passes and fold, with the serial per-pixel loop split
 // over lanes. Micro-tile
@@ -2402,6 +2456,10 @@ struct Lookahead {
   // wave slots the previous launch frees as it drains and never shares the
   // chip with the launch the caller needs next
   int prev[2] = {-1, -1};
+  // bg_waves of the last (trace, fold) kernel pair
+  const void* bg_trace = nullptr;
+  const void* bg_fold = nullptr;
+  uint32_t bg_w = 0;
 };
 
 }  // namespace
@@ -2647,6 +2705,14 @@ FoldFn pick_fold(bool tex, bool mmat, bool lds_materials) {
              : (mmat ? pick_fold2<false, true>(lds_materials) : pick_fold2<false, false>(lds_materials));
 }
 template <bool TEX, bool MMAT>
+FoldFn pick_fold_lite2(bool lds_materials) {
+  return lds_materials ? dev::fold_paths_lite<TEX, MMAT, true> : dev::fold_paths_lite<TEX, MMAT, false>;
+}
+FoldFn pick_fold_lite(bool tex, bool mmat, bool lds_materials) {
+  return tex ? (mmat ? pick_fold_lite2<true, true>(lds_materials) : pick_fold_lite2<true, false>(lds_materials))
+             : (mmat ? pick_fold_lite2<false, true>(lds_materials) : pick_fold_lite2<false, false>(lds_materials));
+}
+template <bool TEX, bool MMAT>
 FoldSplitFn pick_fold_split2(bool lds_materials) {
   return lds_materials ? dev::fold_paths_split<TEX, MMAT, true> : dev::fold_paths_split<TEX, MMAT, false>;
 }
@@ -2787,6 +2853,26 @@ int make_plan(uint32_t owned, uint32_t mpt, uint32_t spp, const fs_options& O, u
   return FS_OK;
 }
 
+// Waves per SIMD of a background (lookahead) trace launch: at most the
+// kernel's bound, and few enough that kBgFoldWaves waves of the fold kernel
+// fit in the SIMD's 512 VGPRs beside them (allocation in blocks of 8): C4 5 of
+// 6 trace waves (80 VGPRs) beside 2 fold waves (50 VGPRs) measured 1744 /
+// 1852 M samples/s in the window loop (lookahead 12 / 24), 3 beside 4 1703 /
+// 1873; C2 6 of 8 (64 VGPRs) 2990 / 3010, 4 3376 / 3419; C3 1166 / 1208 and
+// 1198 / 1211 (profiles/r06/ab_bg_waves.log).
+constexpr int kBgFoldWaves = 4;
+uint32_t bg_waves(LeanFn trace, uint32_t waves, FoldFn fold) {
+  hipFuncAttributes t{}, f{};
+  if (hipFuncGetAttributes(&t, reinterpret_cast<const void*>(trace)) != hipSuccess ||
+      hipFuncGetAttributes(&f, reinterpret_cast<const void*>(fold)) != hipSuccess || t.numRegs <= 0 ||
+      f.numRegs <= 0) {
+    (void)hipGetLastError();
+    return waves;
+  }
+  const int vt = (t.numRegs + 7) / 8 * 8, vf = (f.numRegs + 7) / 8 * 8;
+  return (uint32_t)std::max(1, std::min<int>((int)waves, (512 - kBgFoldWaves * vf) / vt));
+}
+
 // Resident waves per CU of a fold kernel with `lds` bytes of dynamic LDS
 // (the HIP occupancy query on its compiled resources; 28 if it fails).
 uint32_t fold_waves_per_cu(const void* fn, uint32_t lds) {
@@ -2894,7 +2980,7 @@ int fs_options_default(fs_options* o) {
   o->build_log = 0;
   o->persist = 1;
   o->small_mesh_tris = 16;
-  o->lookahead = 12;
+  o->lookahead = 24;
   return FS_OK;
 }
 
@@ -3339,6 +3425,7 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   const uint32_t fold_lds = lm ? 48 * ctx->scene.num_materials : 0;
   const FoldFn fold = pick_fold(tex_rec, mm, lm);
   const FoldSplitFn fold_split = pick_fold_split(tex_rec, mm, lm);
+  const FoldFn fold_lite = pick_fold_lite(tex_rec, mm, lm);
   // Lanes per pixel of the fold: 1 while a launch's micro-tiles fill the
   // fold kernel's resident wave slots at least twice over, else 2 or 4 (a
   // rank's share of a multi-GPU frame), so the serial per-pixel loop is split.
@@ -3369,7 +3456,8 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     Rh.aov_m = (const uint64_t*)A.mid[hit].p + px * hit_group;
     const uint32_t fold_log2 = pblocks >= 2 * fold_slots ? 0u : (pblocks >= fold_slots ? 1u : 2u);
     if (fold_log2 == 0)
-      hipLaunchKernelGGL(fold, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, Lh, Rh);
+      hipLaunchKernelGGL(fold_lite, dim3((uint32_t)pblocks), dim3(kBlock), fold_lds, ctx->stream, ctx->scene, F, Lh,
+                         Rh);
     else
       hipLaunchKernelGGL(fold_split, dim3((uint32_t)(pblocks << fold_log2)), dim3(kBlock), fold_lds, ctx->stream,
                          ctx->scene, F, Lh, Rh, fold_log2);
@@ -3434,7 +3522,16 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       if (A.pending[i]) cov = std::max<uint64_t>(cov, (uint64_t)A.key[i].params.sample_base + (uint64_t)A.groups[i] * spp);
     const uint64_t want = (uint64_t)params->sample_base + (uint64_t)spp * (1 + w);
     const uint64_t pb = (uint64_t)owned * mpt;
-    const uint64_t grid = grid_for(pb * g);
+    // Fewer waves per SIMD than the kernel's bound, so that one wave of the
+    // fold fits beside them on every SIMD: the caller's next fold (context
+    // stream) then runs at once instead of waiting for the launch's waves to
+    // leave (persistent waves leave only when the launch's blocks run out).
+    if (A.bg_trace != reinterpret_cast<const void*>(K.fn) || A.bg_fold != reinterpret_cast<const void*>(fold_lite)) {
+      A.bg_trace = reinterpret_cast<const void*>(K.fn);
+      A.bg_fold = reinterpret_cast<const void*>(fold_lite);
+      A.bg_w = bg_waves(K.fn, K.waves, fold_lite);
+    }
+    const uint64_t grid = std::min<uint64_t>(grid_for(pb * g), (uint64_t)ctx->cus * 4u * A.bg_w);
     const size_t px = (size_t)frame->width * frame->height;
     while (cov < want && cov + (uint64_t)g * spp <= (1ull << 20)) {
       int s = -1;  // the free slot launched longest ago (its stream's last work is the oldest)

@@ -273,11 +273,13 @@ typedef struct fs_options {
                                   one-group launch exceeds it renders in parts of its owned tiles
                                   and, below one tile per part, in launches of fewer samples per
                                   block: frames are identical (ABI 8) */
-  uint32_t lookahead;          /* w calls, 0..48 (12): a render of at most 4 spp over the whole
+  uint32_t lookahead;          /* w calls, 0..48 (24): a render of at most 4 spp over the whole
                                   frame (tile_stride 1, no counters) also traces, in the
                                   background on streams of their own, the samples the next w
                                   calls would add (sample_base + spp, + 2 spp, ...), in launches
-                                  of min(16, max(1, w / 3)) calls each; a later fs_render with the same
+                                  of min(16, max(1, w / 3)) calls each, with fewer waves per
+                                  SIMD than the trace kernel holds so that the caller's folds run
+                                  beside them; a later fs_render with the same
                                   camera, scene, options and parameters and one of those
                                   sample_bases folds its path records instead of tracing, and any
                                   other render discards them. The reference's window loop (one

@@ -49,7 +49,7 @@ def test_options_defaults_and_validation_without_device():
                  "group_major": 0, "tile_order": 1, "xcd_bands": 2, "gpu_bvh_min_tris": 1 << 16, "bvh_leaf": 2,
                  "bvh_bins": 16, "bvh_threads": 0, "node_layout": 0, "build_log": 0, "persist": 1,
                  "small_mesh_tris": 16, "park_lanes_small": 6,
-                 "lds_rows": 1, "record_budget_mb": 0, "lookahead": 12}
+                 "lds_rows": 1, "record_budget_mb": 0, "lookahead": 24}
     assert fsamd.parse_variant("schedule=parked@park_lanes=8") == {"schedule": "parked", "park_lanes": 8}
     assert fsamd.options(schedule="parked").schedule == 2
     lib = fsamd.gpu_lib()

@@ -63,7 +63,7 @@ def test_lookahead_loop_bit_exact(name, spp, scene_dir, gpu_renderer):
 def test_lookahead_discarded_when_the_call_changes(scene_dir, gpu_renderer):
     """A camera change, a skipped sample index and a lens camera between
     calls: a call that changes the camera traces anew (no fold); a skip of
-    one sample index still finds the lookahead (8 calls ahead by default, one
+    one sample index still finds the lookahead (24 calls ahead by default, one
     call with lookahead 1 misses it); a frame reset keeps it. Every frame is
     the oracle's for the same call sequence."""
     s = load_scene("c2", scene_dir)
@@ -138,9 +138,10 @@ def test_frame_map_is_the_plane(scene_dir, gpu_renderer):
 
 
 def test_lookahead_full_width_fold_bit_exact(scene_dir, gpu_renderer):
-    """A frame large enough for the one-lane-per-pixel fold (fold_paths, not
-    the split fold of small frames): four calls, the last three folded from
-    one lookahead launch of four calls, every plane the oracle's."""
+    """A frame large enough for the one-lane-per-pixel fold of a lookahead
+    call (fold_paths_lite, not the split fold of small frames): four calls,
+    the last three folded from one lookahead launch of eight calls (traced with
+    fewer waves per SIMD, bg_waves), every plane the oracle's."""
     s = load_scene("c2", scene_dir)
     cam = s.camera(0)
     gpu_renderer.upload(s)

@@ -72,3 +72,18 @@ def test_every_product_kernel_fits_its_wave_count(resources):
             waves = int(name.split(", ")[1])
             assert r["vgpr_count"] <= 512 // waves // 8 * 8, (name, r)
             assert r["group_segment_fixed_size"] <= 160 * 1024 // (4 * waves), (name, r)
+
+
+def test_lookahead_fold_fits_beside_background_waves():
+    """fold_paths_lite (the fold of a lookahead call) without scratch, in at
+    most 56 VGPRs on untextured scenes (64 textured): bg_waves leaves room for
+    four of its waves per SIMD beside a background trace launch (C4 3 x 80 +
+    4 x 56 <= 512, C2 4 x 64 + 4 x 56), so the window loop's folds never wait
+    for a trace launch to drain."""
+    if not os.path.exists(isa_guard.READELF):
+        pytest.skip("llvm-readelf not in this image")
+    lite = {k: v for k, v in isa_guard.kernel_resources().items() if "fold_paths_lite" in k}
+    assert len(lite) == 8, sorted(lite)
+    for name, r in lite.items():
+        tex = name.startswith("_ZN2fs3dev15fold_paths_liteILb1")
+        assert r["vgpr_count"] <= (64 if tex else 56) and r["private_segment_fixed_size"] == 0, (name, r)
