@@ -129,7 +129,7 @@ for step in "$@"; do
       done
       cat $OUT/dropin_${sc}_1920x1080.json
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
-        -d $OUT/dropin_prof_$sc -o trace -- ./examples/dropin_rate $p 1920 1080 64 > $OUT/dropin_prof_$sc.json \
+        -d $OUT/dropin_prof_$sc -o trace -- ./examples/dropin_rate $p 1920 1080 64 ${la##* } > $OUT/dropin_prof_$sc.json \
         2> $OUT/dropin_prof_$sc.err || fail "$step" $? $OUT/dropin_prof_$sc.err
       python3 tools/dropin_split.py $OUT/dropin_prof_$sc > $OUT/dropin_split_$sc.log 2>&1 || fail "$step" $? $OUT/dropin_split_$sc.log
       cat $OUT/dropin_split_$sc.log ;;
