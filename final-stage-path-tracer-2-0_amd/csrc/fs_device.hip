@@ -2456,6 +2456,17 @@ struct Lookahead {
   // wave slots the previous launch frees as it drains and never shares the
   // chip with the launch the caller needs next
   int prev[2] = {-1, -1};
+  // the last render's key (valid: it could take a lookahead): a render
+  // launches lookahead traces only when it continues that one (same key,
+  // sample_base = the last one's + spp) or folded a lookahead itself, so a
+  // camera that moves every frame starts no background work
+  LookKey last;
+  bool last_valid = false;
+  uint32_t ramp = 0;  // launches since the sequence started (their calls: 1, 2, 4, ... up to g)
+  // a discarded slot's queues were set past every block on the context
+  // stream (its waves stop taking blocks); the slot's next launch waits for it
+  hipEvent_t cancelled[kLookSlots] = {};
+  bool cancel_valid[kLookSlots] = {};
   // bg_waves of the last (trace, fold) kernel pair
   const void* bg_trace = nullptr;
   const void* bg_fold = nullptr;
@@ -2941,7 +2952,7 @@ int fs_destroy(fs_context* ctx) {
   for (int i = 0; i < kLookSlots; i++) {
     Lookahead& A = ctx->la;
     for (DevBuf* b : {&A.rows[i], &A.queues[i], &A.nrm[i], &A.dep[i], &A.mid[i]}) b->release();
-    for (hipEvent_t e : {A.traced[i], A.folded[i], A.kev0[i], A.kev1[i]})
+    for (hipEvent_t e : {A.traced[i], A.folded[i], A.kev0[i], A.kev1[i], A.cancelled[i]})
       if (e) (void)hipEventDestroy(e);
     if (A.stream[i]) (void)hipStreamDestroy(A.stream[i]);
   }
@@ -3407,7 +3418,17 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
     if (!A.pending[i]) continue;
     const uint64_t end = (uint64_t)A.key[i].params.sample_base + (uint64_t)A.groups[i] * A.key[i].params.spp;
     const bool later = hit >= 0 && end > (uint64_t)params->sample_base + params->spp && same_sequence(i);
-    if (!later) A.pending[i] = false;  // the hit slot too once its last call is folded
+    if (later) continue;
+    A.pending[i] = false;  // the hit slot too once its last call is folded
+    if (i != hit) {
+      // Dropped unread: its waves may still trace. Its block queues set past
+      // every block (0x7F7F7F7F) end the launch after the paths in flight (a
+      // launch still waiting for its start zeroes them first and runs out).
+      FS_HIP(hipMemsetAsync(A.queues[i].p, 0x7F, A.queues[i].bytes, ctx->stream));
+      if (!A.cancelled[i]) FS_HIP(hipEventCreateWithFlags(&A.cancelled[i], hipEventDisableTiming));
+      FS_HIP(hipEventRecord(A.cancelled[i], ctx->stream));
+      A.cancel_valid[i] = true;
+    }
   }
   if (hit < 0) A.prev[0] = A.prev[1] = -1;  // a new sequence: no launch to queue behind
   // On an allocation failure the launches shrink (groups per launch, then
@@ -3509,7 +3530,16 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
   // the background in launches of g calls into free slots, after what the
   // pending slots of this sequence already cover; never past the 2^20-sample
   // seed range.
-  if (la_ok) {
+  bool continues = false;  // this call continues the last one's sequence
+  if (la_ok && A.last_valid) {
+    LookKey k = A.last;
+    k.params.sample_base = params->sample_base;
+    continues = (uint64_t)A.last.params.sample_base + A.last.params.spp == params->sample_base &&
+                !std::memcmp(&k, &key, sizeof key);
+  }
+  if (la_ok) A.last = key;
+  A.last_valid = la_ok;
+  if (la_ok && (hit >= 0 || continues)) {
     // g calls per launch: w / 3, so three slots hold the window; at most
     // kLookGroupMax, and fewer where the per-call AOV planes would pass the
     // 32-bit byte offsets of the trace kernel's AOV stores
@@ -3531,9 +3561,15 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       A.bg_fold = reinterpret_cast<const void*>(fold_lite);
       A.bg_w = bg_waves(K.fn, K.waves, fold_lite);
     }
-    const uint64_t grid = std::min<uint64_t>(grid_for(pb * g), (uint64_t)ctx->cus * 4u * A.bg_w);
+    const uint64_t bg_slots = (uint64_t)ctx->cus * 4u * A.bg_w;
     const size_t px = (size_t)frame->width * frame->height;
-    while (cov < want && cov + (uint64_t)g * spp <= (1ull << 20)) {
+    if (hit < 0) A.ramp = 0;  // a sequence starts: its first launches are short
+    for (;;) {
+      // 1, 2, 4, ... calls per launch up to g, so the first calls of a
+      // sequence wait for a short launch rather than a full one
+      const uint32_t gl = std::min<uint32_t>(g, 1u << std::min<uint32_t>(A.ramp, 4));
+      if (!(cov < want && cov + (uint64_t)gl * spp <= (1ull << 20))) break;
+      const uint64_t grid = std::min<uint64_t>(grid_for(pb * gl), bg_slots);
       int s = -1;  // the free slot launched longest ago (its stream's last work is the oldest)
       for (int i = 0; i < kLookSlots; i++)
         if (!A.pending[i] && (s < 0 || A.used[i] < A.used[s])) s = i;
@@ -3548,7 +3584,9 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         FS_HIP(hipEventCreate(&A.kev1[s]));
         if (!A.order) FS_HIP(hipEventCreateWithFlags(&A.order, hipEventDisableTiming));
       }
-      const size_t need = rows_bytes(grid * kBlock, pb * g * spp * kBlock, tex_rec, mm);
+      // (sized for g calls at once, so the ramp does not reallocate)
+      const size_t need = rows_bytes(std::min<uint64_t>(grid_for(pb * g), bg_slots) * kBlock, pb * g * spp * kBlock,
+                                     tex_rec, mm);
       if (A.rows[s].bytes < need || A.nrm[s].bytes < 12 * px * g || A.dep[s].bytes < 4 * px * g ||
           A.mid[s].bytes < 8 * px * g || !A.queues[s].p) {
         FS_HIP(hipStreamSynchronize(A.stream[s]));  // its last trace and folds still use the old buffers
@@ -3559,14 +3597,14 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
           break;
         }
       }
-      if (carve_records(&A.rows[s], grid * kBlock, pb * g * spp * kBlock, &A.R[s], &anchors, tex_rec, mm)) break;
+      if (carve_records(&A.rows[s], grid * kBlock, pb * gl * spp * kBlock, &A.R[s], &anchors, tex_rec, mm)) break;
       Launch Ls = L;
       Ls.owned = owned;
       Ls.tile_offset = 0;
       Ls.sample_base = (uint32_t)cov;
       Ls.spp = spp;
-      Ls.groups = g;
-      Ls.nblocks = (uint32_t)(pb * g);
+      Ls.groups = gl;
+      Ls.nblocks = (uint32_t)(pb * gl);
       Ls.aov_rows = (uint32_t)pb;  // group k's AOVs in plane k
       Ls.aov_plane = (uint32_t)px;
       DevFrame Fs{};  // the trace writes only the AOVs: into the slot's planes
@@ -3581,6 +3619,10 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
         FS_HIP(hipStreamWaitEvent(A.stream[s], A.order, 0));
       }
       if (A.prev[1] >= 0 && A.prev[1] != s) FS_HIP(hipStreamWaitEvent(A.stream[s], A.traced[A.prev[1]], 0));
+      if (A.cancel_valid[s]) {  // the cancel's write lands before this launch zeroes the queues
+        FS_HIP(hipStreamWaitEvent(A.stream[s], A.cancelled[s], 0));
+        A.cancel_valid[s] = false;
+      }
       FS_HIP(hipMemsetAsync(A.queues[s].p, 0, A.queues[s].bytes, A.stream[s]));
       FS_HIP(hipEventRecord(A.kev0[s], A.stream[s]));
       hipLaunchKernelGGL(K.fn, dim3((uint32_t)grid), dim3(kBlock), 0, A.stream[s], ctx->scene, C, Fs, Ls, A.R[s],
@@ -3591,12 +3633,13 @@ int fs_render(fs_context* ctx, const fs_camera* camera, const fs_render_params* 
       A.L[s] = Ls;
       A.key[s] = key;
       A.key[s].params.sample_base = Ls.sample_base;
-      A.groups[s] = g;
+      A.groups[s] = gl;
       A.pending[s] = true;
       A.used[s] = ++A.tick;
       A.prev[1] = A.prev[0];
       A.prev[0] = s;
-      cov += (uint64_t)g * spp;
+      A.ramp++;
+      cov += (uint64_t)gl * spp;
     }
   }
   FS_HIP(hipEventRecord(ctx->ev1, ctx->stream));

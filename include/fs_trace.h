@@ -274,18 +274,21 @@ typedef struct fs_options {
                                   and, below one tile per part, in launches of fewer samples per
                                   block: frames are identical (ABI 8) */
   uint32_t lookahead;          /* w calls, 0..48 (24): a render of at most 4 spp over the whole
-                                  frame (tile_stride 1, no counters) also traces, in the
-                                  background on streams of their own, the samples the next w
-                                  calls would add (sample_base + spp, + 2 spp, ...), in launches
-                                  of min(16, max(1, w / 3)) calls each, with fewer waves per
-                                  SIMD than the trace kernel holds so that the caller's folds run
-                                  beside them; a later fs_render with the same
-                                  camera, scene, options and parameters and one of those
+                                  frame (tile_stride 1, no counters) that continues the previous
+                                  render (same camera, scene, options and parameters, sample_base
+                                  = the previous one's + spp) or folded a lookahead itself also
+                                  traces, in the background on streams of their own, the samples
+                                  the next w calls would add (sample_base + spp, + 2 spp, ...),
+                                  in launches of 1, 2, 4, ... calls up to min(16, max(1, w / 3))
+                                  each, with fewer waves per SIMD than the trace kernel holds so
+                                  that the caller's folds run beside them; a later fs_render with
+                                  the same camera, scene, options and parameters and one of those
                                   sample_bases folds its path records instead of tracing, and any
-                                  other render discards them. The reference's window loop (one
-                                  TraceScene per displayed frame, main.cpp:157-163) then keeps the
-                                  GPU busy while the host reads each frame. Frames are identical;
-                                  0 off (ABI 9) */
+                                  other render discards them (their launches stop taking work).
+                                  The reference's window loop (one TraceScene per displayed
+                                  frame, main.cpp:157-163) then keeps the GPU busy while the host
+                                  reads each frame; a camera that moves every frame starts no
+                                  background work. Frames are identical; 0 off (ABI 9) */
 } fs_options;
 
 /* ---- context ---------------------------------------------------------- */

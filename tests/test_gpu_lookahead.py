@@ -1,8 +1,9 @@
 """The lookahead of small renders (fs_options.lookahead, ABI 9): a whole-frame
-render of at most 4 spp also traces the next call's samples in the background;
-the next call folds them. Frames must be those of the plain loop, bit for bit
-against the oracle, whatever the caller does between calls (camera change,
-frame reset, re-upload, another frame, a gap in sample_base)."""
+render of at most 4 spp that continues the previous call's sequence also traces
+the next calls' samples in the background; those calls fold them. Frames must
+be those of the plain loop, bit for bit against the oracle, whatever the caller
+does between calls (camera change, frame reset, re-upload, another frame, a gap
+in sample_base, a sequence dropped while its traces still run)."""
 import numpy as np
 import pytest
 
@@ -42,16 +43,17 @@ def gpu_seq(r, frame, steps, reset_at=()):
 
 @pytest.mark.parametrize("name,spp", [("c2", 1), ("c4", 1), ("c2", 3)])
 def test_lookahead_loop_bit_exact(name, spp, scene_dir, gpu_renderer):
-    """N calls of spp samples each (TraceScene's loop): every call after the
-    first folds the lookahead, and the frame (colour, count, display and the
-    last sample's normal / depth / material) equals the oracle's."""
+    """N calls of spp samples each (TraceScene's loop): the second call
+    continues the first and starts the lookahead, every later call folds it,
+    and the frame (colour, count, display and the last sample's normal / depth
+    / material) equals the oracle's."""
     s = load_scene(name, scene_dir)
     cam = s.camera(0)
     gpu_renderer.upload(s)
     f = gpu_renderer.frame(W, H)
     steps = [(cam, spp, k * spp) for k in range(5)]
     folded = gpu_seq(gpu_renderer, f, steps)
-    assert folded == [False, True, True, True, True]
+    assert folded == [False, False, True, True, True]
     assert gpu_renderer.last_launches() == (1, spp)
     assert gpu_renderer.last_trace_ms() > 0
     out = planes(f)
@@ -62,10 +64,11 @@ def test_lookahead_loop_bit_exact(name, spp, scene_dir, gpu_renderer):
 
 def test_lookahead_discarded_when_the_call_changes(scene_dir, gpu_renderer):
     """A camera change, a skipped sample index and a lens camera between
-    calls: a call that changes the camera traces anew (no fold); a skip of
-    one sample index still finds the lookahead (24 calls ahead by default, one
-    call with lookahead 1 misses it); a frame reset keeps it. Every frame is
-    the oracle's for the same call sequence."""
+    calls: a call that changes the camera traces anew (no fold, and starts no
+    lookahead until the next call continues it); a skip of one sample index
+    still finds the lookahead (24 calls ahead by default; with lookahead 1 it
+    misses); a frame reset keeps it. Every frame is the oracle's for the same
+    call sequence."""
     s = load_scene("c2", scene_dir)
     a = s.camera(0)
     b = fsamd.camera((2, 9, -30), (0, 10, 0), fov_y=44, aperture=0.0)
@@ -74,18 +77,19 @@ def test_lookahead_discarded_when_the_call_changes(scene_dir, gpu_renderer):
     f = gpu_renderer.frame(W, H)
     steps = [(a, 1, 0), (a, 1, 1), (b, 1, 2), (b, 1, 3), (b, 1, 5), (b, 1, 6), (lens, 1, 7), (lens, 1, 8)]
     folded = gpu_seq(gpu_renderer, f, steps)
-    assert folded == [False, True, False, True, True, True, False, True]
+    assert folded == [False, False, False, False, True, True, False, False]
     gpu_renderer.set_options(lookahead=1)  # depth 1: the skip misses
-    folded = gpu_seq(gpu_renderer, f, [(a, 1, 9), (a, 1, 10), (a, 1, 12), (a, 1, 13)])
-    assert folded == [False, True, False, True]
-    steps += [(a, 1, 9), (a, 1, 10), (a, 1, 12), (a, 1, 13)]
+    more = [(a, 1, 9), (a, 1, 10), (a, 1, 11), (a, 1, 13), (a, 1, 14)]
+    folded = gpu_seq(gpu_renderer, f, more)
+    assert folded == [False, False, True, False, False]
+    steps += more
     gpu_renderer.set_options(lookahead=2)
     out = planes(f)
     assert_parity(out, oracle_seq(s.desc_ptr(), steps), exact=True)
     # a reset between two calls of the same sequence: the fold goes into the reset frame
     steps2 = [(a, 1, 0), (a, 1, 1), (a, 1, 2)]
     folded = gpu_seq(gpu_renderer, f, steps2, reset_at=(2,))
-    assert folded == [False, True, True]
+    assert folded == [False, False, True]
     out = planes(f)
     f.close()
     assert_parity(out, oracle_seq(s.desc_ptr(), [(a, 1, 2)]), exact=True)
@@ -100,13 +104,16 @@ def test_lookahead_after_reupload_and_across_frames(scene_dir, gpu_renderer):
     gpu_renderer.upload(s2)
     f = gpu_renderer.frame(W, H)
     gpu_renderer.render(cam, f, spp=1, sample_base=0)
-    gpu_renderer.upload(s2)  # same scene, new upload: the pending trace is dropped
-    gpu_renderer.render(cam, f, spp=1, sample_base=1)
-    assert not gpu_renderer.last_lookahead()
+    gpu_renderer.render(cam, f, spp=1, sample_base=1)  # starts a lookahead
+    gpu_renderer.upload(s2)  # same scene, new upload: the pending traces are dropped
     gpu_renderer.render(cam, f, spp=1, sample_base=2)
+    assert not gpu_renderer.last_lookahead()
+    gpu_renderer.render(cam, f, spp=1, sample_base=3)
+    assert not gpu_renderer.last_lookahead()
+    gpu_renderer.render(cam, f, spp=1, sample_base=4)
     assert gpu_renderer.last_lookahead()
     out = planes(f)
-    assert_parity(out, oracle_seq(s2.desc_ptr(), [(cam, 3, 0)]), exact=True)
+    assert_parity(out, oracle_seq(s2.desc_ptr(), [(cam, 5, 0)]), exact=True)
     g = gpu_renderer.frame(W, H)
     f.reset()
     for k in range(3):  # f and g each get samples 0, 1, 2
@@ -140,7 +147,7 @@ def test_frame_map_is_the_plane(scene_dir, gpu_renderer):
 def test_lookahead_full_width_fold_bit_exact(scene_dir, gpu_renderer):
     """A frame large enough for the one-lane-per-pixel fold of a lookahead
     call (fold_paths_lite, not the split fold of small frames): four calls,
-    the last three folded from one lookahead launch of eight calls (traced with
+    the last two folded from one lookahead launch of eight calls (traced with
     fewer waves per SIMD, bg_waves), every plane the oracle's."""
     s = load_scene("c2", scene_dir)
     cam = s.camera(0)
@@ -151,10 +158,35 @@ def test_lookahead_full_width_fold_bit_exact(scene_dir, gpu_renderer):
     for k in range(4):
         gpu_renderer.render(cam, f, spp=1, sample_base=k)
         folded.append(gpu_renderer.last_lookahead())
-    assert folded == [False, True, True, True]
+    assert folded == [False, False, True, True]
     out = planes(f)
     f.close()
     o = oracle_py.Scene(s.desc_ptr())
     ref = o.render(cam, fsamd.render_params(w, h, 4), threads=16)
     o.close()
     assert_parity(out, ref, exact=True)
+
+
+def test_dropped_sequences_reuse_their_slots_bit_exact(scene_dir, gpu_renderer):
+    """Sequences dropped while their background traces still run (C4, window
+    24: the dropped launches' queues are cancelled on the context stream) and
+    new sequences launched into the same slots at once, several times over:
+    the folds of the new sequences read only their own traces, and the frame
+    equals the oracle's for the same calls."""
+    s = load_scene("c4", scene_dir)
+    a = s.camera(0)
+    b = fsamd.camera((2, 9, -30), (0, 10, 0), fov_y=44, aperture=0.0)
+    gpu_renderer.upload(s)
+    gpu_renderer.set_options(lookahead=24)
+    f = gpu_renderer.frame(W, H)
+    steps, folded = [], []
+    for rnd in range(3):
+        cam = (a, b)[rnd % 2]
+        seq = [(cam, 1, k) for k in range(5)]
+        f.reset()
+        folded += gpu_seq(gpu_renderer, f, seq)
+        steps = seq
+    assert folded == [False, False, True, True, True] * 3
+    out = planes(f)
+    f.close()
+    assert_parity(out, oracle_seq(s.desc_ptr(), steps), exact=True)

@@ -37,11 +37,12 @@ def main(root):
     if len(folds) < 8:
         raise SystemExit(f"only {len(folds)} folds in {root}")
     # frame k: fold k and the first display copy after it; the k-th trace made
-    # its samples (traces start in sample order). Skip the warm-up frame and
-    # the batched submission at the end (its fold has no copy before the last).
+    # its samples (traces start in sample order). Skip the two warm-up frames
+    # (dropin_rate's untimed calls) and the batched submission at the end (its
+    # fold has no copy before the last).
     frames = []
     ci = 0
-    for k in range(1, len(folds) - 2):
+    for k in range(2, len(folds) - 2):
         fs, fe = folds[k]
         while ci < len(copies) and copies[ci][0] < fe:
             ci += 1
