@@ -403,7 +403,7 @@ static void node_add_face(onode* n, uint32_t f) {
 
 /* bvh.h:108-137 */
 static void configure_children(omesh* m, uint32_t ni) {
-  v3 mn = m->nodes[ni].aabb.mn, mx = m->nodes[ni].aabb.mx;
+  v3 mn = m->nodes[ni].aabb.mn;
   v3 center = bounds_center(&m->nodes[ni].aabb);
   v3 hx = sub3(mk3(center.x, mn.y, mn.z), mn);
   v3 hy = sub3(mk3(mn.x, center.y, mn.z), mn);
